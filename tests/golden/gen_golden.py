@@ -1,0 +1,284 @@
+"""Generate the golden fixtures from the REAL reference generate() (survey container only).
+
+This script imports the reference from /root/reference (read-only) with three import shims
+(SURVEY.md §8c), injects the Philox noise contract of oracle/philox.py into its sampler, runs
+``WaveRNN.generate`` / ``vocoder.inference.infer_waveform`` on seeded synthetic weights and
+mels, and writes small .npz fixtures next to this file. The fixtures are data (inputs are
+regenerated from the recorded seeds; outputs are the reference's labels / samples / waveform)
+so the GPU box never needs the reference.
+
+It also re-runs the oracle restatement (oracle/wavernn_oracle.py) on the same inputs and
+asserts it is bit-identical to the reference, which pins the oracle.
+
+Usage:  python tests/golden/gen_golden.py [--only NAME] [--threads N]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'real-time-voice-cloning_amd'))
+
+import torch  # noqa: E402
+
+from oracle import philox  # noqa: E402
+from oracle.wavernn_oracle import oracle_infer_waveform  # noqa: E402
+from wavernn_amd.synth import synth_state_dict, synth_mel  # noqa: E402
+
+# name: (model_type, mode, bits, T, batched, target, overlap, weight_seed, mel_seed, logit_scale,
+#        noise_seed, record_logit_steps)
+CASES = {
+    'fatchord_raw9_tiny': ('fatchord-wavernn', 'RAW', 9, 24, True, 1000, 100, 1, 11, 1.0, 101,
+                           [0, 1, 2, 500, 1199]),
+    'fatchord_raw9_sharp_tiny': ('fatchord-wavernn', 'RAW', 9, 24, True, 1000, 100, 2, 12, 8.0,
+                                 102, [0, 1, 600]),
+    'fatchord_mol_tiny': ('fatchord-wavernn', 'MOL', 9, 24, True, 1000, 100, 3, 13, 1.0, 103,
+                          [0, 1, 700]),
+    'runtimeracer_raw9_tiny': ('runtimeracer-wavernn', 'RAW', 9, 24, True, 1000, 100, 4, 14, 1.0,
+                               104, [0, 1, 800]),
+    'runtimeracer_mol_tiny': ('runtimeracer-wavernn', 'MOL', 9, 24, True, 1000, 100, 5, 15, 1.0,
+                              105, [0, 3]),
+    'fatchord_raw10_unbatched_tiny': ('fatchord-wavernn', 'RAW', 10, 22, False, None, None, 6, 16,
+                                      1.0, 106, [0, 5, 4399]),
+    'fatchord_raw10_defaults': ('fatchord-wavernn', 'RAW', 10, 53, True, None, None, 7, 17, 1.0,
+                                107, [0]),
+    'runtimeracer_raw10_defaults': ('runtimeracer-wavernn', 'RAW', 10, 71, True, None, None, 8,
+                                    18, 1.0, 108, [0]),
+    # BASELINE.json configs[0]: 200-frame random mel, mu-law 9-bit, target=11000 overlap=550
+    'fatchord_raw9_config1': ('fatchord-wavernn', 'RAW', 9, 200, True, 11000, 550, 0, 0, 1.0, 0,
+                              [0, 1, 6000, 12099]),
+}
+
+
+def install_shims():
+    """np.cumproduct, librosa/soundfile stubs, WaveRNNVocoder stub."""
+    if not hasattr(np, 'cumproduct'):
+        np.cumproduct = np.cumprod
+    for name in ('librosa', 'soundfile', 'WaveRNNVocoder'):
+        if name not in sys.modules:
+            sys.modules[name] = types.ModuleType(name)
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+class NoiseState:
+    seed = 0
+    stream = 0
+    step = 0
+
+
+class PatchedCategorical:
+    """torch.distributions.Categorical with the Exp(1) draw replaced by the Philox contract.
+
+    torch 2.10: Categorical.__init__ normalises ``probs / probs.sum(-1, keepdim=True)``;
+    sample() -> multinomial(probs, 1, True) -> ``argmax(probs / q)``, q ~ Exp(1).
+    """
+
+    def __init__(self, probs=None, logits=None, validate_args=None):
+        self.probs = probs / probs.sum(-1, keepdim=True)
+
+    def sample(self, sample_shape=torch.Size()):
+        B, n = self.probs.shape
+        q = philox.raw_exp_noise(NoiseState.seed, NoiseState.stream, [NoiseState.step],
+                                 np.arange(B), n)[0]
+        NoiseState.step += 1
+        return torch.argmax(self.probs / torch.from_numpy(q), dim=-1)
+
+
+def check_multinomial_identity():
+    """Self-test of the identity the patch relies on (torch 2.10 CPU)."""
+    for seed in range(5):
+        p = torch.softmax(torch.randn(6, 512) * 2, dim=1)
+        p = p / p.sum(-1, keepdim=True)
+        torch.manual_seed(seed)
+        real = torch.multinomial(p, 1, True).view(-1)
+        torch.manual_seed(seed)
+        q = torch.empty_like(p).exponential_(1)
+        mine = torch.argmax(p / q, dim=-1)
+        assert torch.equal(real, mine), 'multinomial fast-path identity does not hold'
+
+
+def make_mol_patch(orig):
+    def patched(y, log_scale_min=None):
+        B = y.size(2)
+        u1, u2 = philox.mol_uniforms(NoiseState.seed, NoiseState.stream, [NoiseState.step],
+                                     np.arange(B))
+        vals = iter([torch.from_numpy(u1[0][None].copy()), torch.from_numpy(u2[0][None].copy())])
+        real_uniform = torch.Tensor.uniform_
+
+        def fake_uniform_(self, a=0.0, b=1.0, generator=None):
+            v = next(vals)
+            assert tuple(v.shape) == tuple(self.shape), (v.shape, self.shape)
+            assert a == philox.MOL_LO and b == philox.MOL_HI
+            self.copy_(v)
+            return self
+
+        torch.Tensor.uniform_ = fake_uniform_
+        try:
+            r = orig(y, log_scale_min)
+        finally:
+            torch.Tensor.uniform_ = real_uniform
+        NoiseState.step += 1
+        return r
+    return patched
+
+
+def ref_hparams(model_type, mode, bits):
+    from config import hparams as H
+    import copy
+    base = H.wavernn_fatchord if model_type == 'fatchord-wavernn' else H.wavernn_runtimeracer
+    hp = copy.deepcopy(base)
+    hp.mode = mode
+    hp.bits = bits
+    return hp
+
+
+def run_reference(name, case):
+    (model_type, mode, bits, T, batched, target, overlap, wseed, mseed, lscale, nseed,
+     rec_steps) = case
+    install_shims()
+    from vocoder.models import base
+    import vocoder.models.fatchord_version as fv
+    import vocoder.models.runtimeracer_version as rv
+    import vocoder.inference as vinf
+
+    hp = ref_hparams(model_type, mode, bits)
+    if model_type == 'fatchord-wavernn':
+        model, _ = base.init_voc_model(model_type, torch.device('cpu'), override_hp_fatchord=hp)
+    else:
+        model, _ = base.init_voc_model(model_type, torch.device('cpu'),
+                                       override_hp_runtimeracer=hp)
+    sd_np = synth_state_dict(hp, model_type, seed=wseed, logit_scale=lscale)
+    ref_sd = model.state_dict()
+    new_sd = {}
+    for k, v in ref_sd.items():
+        if k.endswith('num_batches_tracked'):
+            new_sd[k] = torch.zeros_like(v)
+        else:
+            assert k in sd_np, k
+            assert tuple(sd_np[k].shape) == tuple(v.shape), (k, sd_np[k].shape, v.shape)
+            new_sd[k] = torch.from_numpy(sd_np[k].copy())
+    assert set(sd_np) == set(k for k in ref_sd if not k.endswith('num_batches_tracked'))
+    model.load_state_dict(new_sd)
+    model = model.eval()
+
+    # vocoder.inference singletons (inference.py:7-8) -> drive infer_waveform itself
+    vinf._model = model
+    vinf._model_type = model_type
+    hp_name = 'wavernn_fatchord' if model_type == 'fatchord-wavernn' else 'wavernn_runtimeracer'
+    setattr(vinf, hp_name, hp)
+
+    last_fc = model.fc3 if model_type == 'fatchord-wavernn' else model.fc5
+    rec = {}
+
+    def hook(mod, inp, out):
+        if NoiseState.step in rec_steps and out.dim() == 2:
+            rec[NoiseState.step] = out.detach().clone().numpy()
+    hnd = last_fc.register_forward_hook(hook)
+
+    mel = synth_mel(T, seed=mseed)
+    NoiseState.seed, NoiseState.stream, NoiseState.step = nseed, 0, 0
+    real_cat = torch.distributions.Categorical
+    torch.distributions.Categorical = PatchedCategorical
+    fv_orig, rv_orig = fv.sample_from_discretized_mix_logistic, rv.sample_from_discretized_mix_logistic
+    fv.sample_from_discretized_mix_logistic = make_mol_patch(fv_orig)
+    rv.sample_from_discretized_mix_logistic = make_mol_patch(rv_orig)
+    captured = {}
+    orig_stack = torch.stack
+
+    def spy_stack(tensors, *a, **k):
+        r = orig_stack(tensors, *a, **k)
+        if len(tensors) > 50 and tensors[0].dim() == 1:
+            captured['samples'] = r.transpose(0, 1).clone().numpy()
+        return r
+    t0 = time.time()
+    try:
+        torch.stack = spy_stack
+        wav = vinf.infer_waveform(mel, normalize=True, batched=batched, target=target,
+                                  overlap=overlap, progress_callback=lambda *a: None)
+    finally:
+        torch.stack = orig_stack
+        torch.distributions.Categorical = real_cat
+        fv.sample_from_discretized_mix_logistic = fv_orig
+        rv.sample_from_discretized_mix_logistic = rv_orig
+        hnd.remove()
+    dt = time.time() - t0
+    model.eval()
+    samples = captured['samples']
+    res = dict(wav=np.asarray(wav, dtype=np.float64), samples=samples.astype(np.float32),
+               steps=NoiseState.step, t=dt)
+    if mode == 'RAW':
+        n = 2 ** bits
+        # labels recovered exactly from the fp32 samples: sample = 2k/(n-1) - 1 (fp32)
+        ks = np.arange(n, dtype=np.float32)
+        table = (np.float32(2) * ks) / np.float32(n - 1.) - np.float32(1.)
+        lab = np.searchsorted(table, samples)
+        assert np.array_equal(table[lab], samples)
+        res['labels'] = lab.astype(np.int16)
+    res['logits'] = rec
+    return hp, sd_np, mel, res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--only', default=None)
+    ap.add_argument('--threads', type=int, default=8)
+    args = ap.parse_args()
+    torch.set_num_threads(args.threads)
+    install_shims()
+    check_multinomial_identity()
+    meta_all = {}
+    meta_path = os.path.join(HERE, 'golden_meta.json')
+    if os.path.exists(meta_path):
+        meta_all = json.load(open(meta_path))
+    for name, case in CASES.items():
+        if args.only and name not in args.only.split(','):
+            continue
+        (model_type, mode, bits, T, batched, target, overlap, wseed, mseed, lscale, nseed,
+         rec_steps) = case
+        hp, sd, mel, res = run_reference(name, case)
+        tgt = hp.gen_target if target is None else target
+        ovl = hp.gen_overlap if overlap is None else overlap
+        # oracle restatement on the same inputs must be bit-identical
+        t0 = time.time()
+        o = oracle_infer_waveform(sd, hp, model_type, mel, batched=batched, target=tgt,
+                                  overlap=ovl, seed=nseed, stream=0,
+                                  record_logits=set(rec_steps))
+        t_or = time.time() - t0
+        same_wav = np.array_equal(o['wav'], res['wav'])
+        same_samples = np.array_equal(o['samples'], res['samples'])
+        same_labels = (mode != 'RAW') or np.array_equal(o['labels'], res['labels'])
+        same_logits = all(np.array_equal(o['logits'][s], res['logits'][s]) for s in rec_steps)
+        print(f"{name}: B={o['B']} S={o['S']} ref {res['t']:.1f}s oracle {t_or:.1f}s "
+              f"wav_eq={same_wav} samples_eq={same_samples} labels_eq={same_labels} "
+              f"logits_eq={same_logits}", flush=True)
+        assert same_wav and same_samples and same_labels and same_logits, name
+        out = dict(wav=res['wav'], logits_steps=np.array(rec_steps, dtype=np.int64),
+                   logits=np.stack([res['logits'][s] for s in rec_steps]).astype(np.float32))
+        if mode == 'RAW':
+            out['labels'] = res['labels']
+        else:
+            out['samples'] = res['samples']
+        np.savez_compressed(os.path.join(HERE, name + '.npz'), **out)
+        meta_all[name] = dict(model_type=model_type, mode=mode, bits=bits, n_frames=T,
+                              batched=batched, target=tgt, overlap=ovl, weight_seed=wseed,
+                              mel_seed=mseed, logit_scale=lscale, noise_seed=nseed, stream=0,
+                              num_folds=int(o['B']), seq_len=int(o['S']),
+                              wave_len=int(len(res['wav'])), ref_seconds=round(res['t'], 2))
+    meta_all['_env'] = dict(torch=torch.__version__, numpy=np.__version__,
+                            threads=args.threads, generator='tests/golden/gen_golden.py',
+                            reference='/root/reference @ 2025-02-27 (RuntimeRacer/Real-Time-Voice-Cloning)')
+    with open(meta_path, 'w') as f:
+        json.dump(meta_all, f, indent=1, sort_keys=True)
+
+
+if __name__ == '__main__':
+    main()
