@@ -1,0 +1,148 @@
+/*
+ * wavernn_mi355x.h -- C-ABI of the MI355X-native WaveRNN vocoder (libwavernn_mi355x.so).
+ *
+ * Drop-in boundary for the reference's vocoder inference path. Each entry point names the
+ * reference interface it replaces (paths relative to RuntimeRacer/Real-Time-Voice-Cloning):
+ *
+ *   reference                                                   this ABI
+ *   -----------------------------------------------------------  -------------------------------
+ *   WaveRNNVocoder.Vocoder()        libwavernn/<variant>/src/     wrnn_create
+ *                                   WaveRNNVocoder.cpp:17-21
+ *   Vocoder.loadWeights(path)       WaveRNNVocoder.cpp:22-31       wrnn_load_tensor + wrnn_finalize
+ *   model.load_state_dict(sd)       vocoder/inference.py:35        (state-dict names, PyTorch layout)
+ *   Vocoder.setRandomSeed(seed)     WaveRNNVocoder.cpp:33-35       wrnn_set_seed
+ *   torch.manual_seed(seed)         vocoder/inference.py:97-101
+ *   Vocoder.melToWav(mels)          WaveRNNVocoder.cpp:37-47       wrnn_generate (host buffers)
+ *   WaveRNN.generate(mels, batched, vocoder/models/                 wrnn_generate / _device
+ *     target, overlap, ...)         fatchord_version.py:155-240    (device loop; the f64 cross-fade,
+ *                                   runtimeracer_version.py:199-295 mu-law and de-emphasis stay on
+ *                                                                   the host, :242-255)
+ *   fold_with_overlap arithmetic    fatchord_version.py:316-327    wrnn_fold_shape
+ *   RuntimeError("Model hasn't been loaded ...")  WaveRNNVocoder.cpp:39-41   WRNN_ERR_NOT_LOADED +
+ *   RuntimeError("Cannot open file.")             WaveRNNVocoder.cpp:24-26   wrnn_last_error()
+ *
+ * Conventions: plain C types only; every function returns 0 on success and a negative
+ * WRNN_ERR_* code on failure, with a thread-local message from wrnn_last_error(). Nothing
+ * throws or aborts across the ABI. A handle owns its device memory and HIP stream and must be
+ * used by one thread at a time; distinct handles are independent (one per GPU / per caller
+ * thread), unlike the reference's shared static RNG (net_impl.cpp:136).
+ *
+ * Sampling noise follows the Philox4x32-10 contract documented in DESIGN.md ("RNG contract"):
+ * identical (seed, stream) -> identical outputs on any device.
+ */
+#ifndef WAVERNN_MI355X_H
+#define WAVERNN_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WRNN_OK 0
+#define WRNN_ERR_INVALID (-1)    /* bad argument / unsupported hyper-parameters        */
+#define WRNN_ERR_NOT_LOADED (-2) /* generate before finalize (WaveRNNVocoder.cpp:39-41) */
+#define WRNN_ERR_HIP (-3)        /* HIP runtime error                                   */
+#define WRNN_ERR_OOM (-4)        /* device allocation failed                            */
+#define WRNN_ERR_ABORTED (-5)    /* progress callback returned non-zero                 */
+#define WRNN_ERR_CAPACITY (-6)   /* caller's output buffer too small                    */
+
+#define WRNN_MODEL_FATCHORD 0     /* 'fatchord-wavernn'     vocoder/models/base.py:13 */
+#define WRNN_MODEL_RUNTIMERACER 1 /* 'runtimeracer-wavernn' vocoder/models/base.py:15 */
+
+#define WRNN_MODE_RAW 0 /* softmax over 2**bits classes, Categorical sample */
+#define WRNN_MODE_MOL 1 /* 10-component discretized mixture of logistics   */
+
+/* Topology, with the field names of config/hparams.py:220-285 / :356-421. */
+typedef struct wrnn_config {
+    int model_type;         /* WRNN_MODEL_*                         */
+    int mode;               /* WRNN_MODE_*                          */
+    int bits;               /* RAW: n_classes = 2**bits             */
+    int rnn_dims;           /* 512 fatchord, 256 runtimeracer       */
+    int fc_dims;
+    int compute_dims;       /* MelResNet width (128)                */
+    int res_out_dims;       /* aux width (128); aux_dims = /4       */
+    int res_blocks;         /* 10                                   */
+    int pad;                /* 2                                    */
+    int feat_dims;          /* num_mels (80)                        */
+    int hop_length;         /* 200 = prod(upsample_factors)         */
+    int n_upsample;         /* number of upsample stages (3)        */
+    int upsample_factors[4];/* (5, 5, 8)                            */
+} wrnn_config;
+
+typedef struct wrnn_handle wrnn_handle;
+
+/* Called every 100 steps with the reference's progress_callback arguments
+ * (fatchord_version.py:234-236): step index i, seq_len, b_size, gen_rate in kHz.
+ * Return non-zero to abort generation (WRNN_ERR_ABORTED). */
+typedef int (*wrnn_progress_fn)(void* user, int i, int seq_len, int b_size, double gen_rate_khz);
+
+/* Library / device info. */
+const char* wrnn_version(void);
+const char* wrnn_last_error(void);
+int wrnn_device_count(int* count);
+
+/* Create a vocoder bound to HIP device `device`. */
+int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out);
+void wrnn_destroy(wrnn_handle* h);
+
+/* Load one state-dict tensor (fp32, PyTorch layout/shape, host memory); names as in the
+ * reference state_dict, e.g. "rnn1.weight_ih_l0", "upsample.resnet.conv_in.weight".
+ * Unknown names (e.g. "step") are ignored; shape mismatches are WRNN_ERR_INVALID. */
+int wrnn_load_tensor(wrnn_handle* h, const char* name, const float* data, const int64_t* shape,
+                     int ndim);
+/* Check every required tensor is present and repack them into the device layout. */
+int wrnn_finalize(wrnn_handle* h);
+
+/* Seed of the Philox noise; resets the per-call stream counter (torch.manual_seed). */
+int wrnn_set_seed(wrnn_handle* h, uint64_t seed);
+/* Explicit stream id for the next call (advanced by one per utterance afterwards). */
+int wrnn_set_stream(wrnn_handle* h, uint32_t stream);
+
+/* Fold arithmetic of fold_with_overlap for a mel of n_frames frames
+ * (upsampled length L = n_frames * hop). batched=0 -> one row of L steps. */
+int wrnn_fold_shape(int n_frames, int hop_length, int batched, int target, int overlap,
+                    int* num_folds, int* seq_len);
+
+/* Generate one utterance. mel: host float32 (feat_dims, n_frames) row-major, ALREADY
+ * normalised (divided by max_abs_value, vocoder/inference.py:91-92).
+ * Outputs per fold row, row-major (num_folds, seq_len):
+ *   RAW: labels[b*seq_len+i] (int16 class index) and/or samples (float32 2k/(n-1)-1)
+ *   MOL: samples (float32 in [-1, 1]); labels must be NULL.
+ * `capacity` = elements available in each non-NULL output buffer. */
+int wrnn_generate(wrnn_handle* h, const float* mel, int n_frames, int batched, int target,
+                  int overlap, int16_t* labels, float* samples, size_t capacity,
+                  int* num_folds, int* seq_len, wrnn_progress_fn cb, void* user);
+
+/* Batched multi-utterance generation with inputs resident in HBM: mels[u] are DEVICE
+ * pointers to (feat_dims, n_frames[u]) float32. Rows of all utterances run as one batch of
+ * sum(num_folds) rows; row_offset[u] (host, n_utts+1 entries, filled by the call) gives each
+ * utterance's first row. Outputs are DEVICE buffers of (total_rows, seq_len). Utterance u
+ * uses noise stream (stream + u). Results are identical to n_utts single calls. */
+int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* mels,
+                               const int* n_frames, int batched, int target, int overlap,
+                               int16_t* labels_dev, float* samples_dev, size_t capacity,
+                               int* row_offset, int* seq_len, wrnn_progress_fn cb, void* user);
+
+/* Per-stage timing of the dominant recurrent kernel (in-kernel s_memrealtime stamps,
+ * 100 MHz). Enable before a call; read after: average duration in microseconds of the
+ * launches of stage `stage` in the last call, and the number of launches averaged. */
+int wrnn_enable_stage_timing(wrnn_handle* h, int enable);
+int wrnn_stage_timing(wrnn_handle* h, int stage, double* avg_us, int* launches);
+/* Name and algorithmic bytes / FLOPs per launch of stage `stage` for the last call's shape. */
+int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, double* bytes,
+                    double* flops, int* n_stages);
+
+/* Raw access for tests: copy the RAW noise (seq_len, rows, n_classes) of the last call's
+ * first `n_steps` steps to host (float32). */
+int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity);
+/* Copy the upsampled conditioning of the last call to host: mel (L, feat) and aux
+ * (n_frames, res_out_dims) per utterance 0. */
+int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* aux_out,
+                        size_t aux_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAVERNN_MI355X_H */

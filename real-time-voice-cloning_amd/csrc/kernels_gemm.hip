@@ -1,0 +1,142 @@
+// GEMM-shaped precompute of the vocoder: the MelResNet convolutions of the upsample network
+// (reference vocoder/models/fatchord_version.py:9-44) and the conditioning products that the
+// recurrence consumes every step (the aux/mel parts of I, rnn2/rnn3, fc1..fc3 input concats,
+// fatchord_version.py:198-211). These are the dense contractions of the path, so they run on
+// the fp32 matrix cores: v_mfma_f32_32x32x2_f32 (exact f32, an fma chain in k order).
+//
+// D[m][n] = sum_k A(m,k) B(k,n): 64x64 workgroup tile, 4 waves of 32x32, BK = 16 staged in LDS
+// as [k][m] / [k][n] so each MFMA operand read is one conflict-free 32-lane row.
+// Also here: the stretch + box-conv stencils of the mel upsampler (fatchord_version.py:47-85).
+#include "wrnn_kernels.h"
+
+namespace wrnn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float load_a(const GemmA& a, int m, int k) {
+    switch (a.kind) {
+        case 0:
+            return a.p[(size_t)m * a.ld + k];
+        case 1: {  // cI: [mel_up(p) (n_mel) | aux(p // hop)[r_off : r_off + n_aux]]
+            if (m >= a.L) return 0.f;
+            if (k < a.n_mel) return a.mel[(size_t)k * a.ldm + m];
+            return a.R[(size_t)(a.r_off + k - a.n_mel) * a.ldr + m / a.hop];
+        }
+        default: {  // frame-A: slot 0 is the zero frame; slot f+1 = frame f
+            if (m == 0) return 0.f;
+            return a.R[(size_t)(a.r_off + k) * a.ldr + (m - 1)];
+        }
+    }
+}
+
+__device__ __forceinline__ float load_b(const GemmB& b, int k, int n) {
+    if (b.kind == 0) return b.p[(size_t)k * b.ld + n];
+    // im2col of the zero-padded mel (pad_tensor(.., pad, 'both'), fatchord_version.py:171)
+    const int ci = k / b.ksz, kk = k % b.ksz;
+    const int i = n + kk - b.pad;
+    return (i >= 0 && i < b.T) ? b.p[(size_t)ci * b.T + i] : 0.f;
+}
+
+__device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float acc) {
+    float v;
+    switch (e.kind) {
+        case 0:
+            v = acc + e.bias[n];
+            break;
+        case 1:
+            v = acc + e.bias[m];
+            break;
+        default: {
+            // eval BatchNorm as torch CPU: x * (w / sqrt(var + eps)) + (b - mean * alpha)
+            v = fmaf(acc, e.alpha[m], e.beta[m]);
+            if (e.relu) v = v > 0.f ? v : 0.f;
+            if (e.res) v = v + e.res[(size_t)m * e.ld + n];
+            break;
+        }
+    }
+    e.D[(size_t)m * e.ld + n] = v;
+}
+
+__global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
+                                                   GemmEp E) {
+    __shared__ float As[16][64];
+    __shared__ float Bs[16][64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv & 1, wn = wv >> 1;
+    const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + i * kThreads;
+            const int mm = e & 63, kk = e >> 6;
+            const int m = m0 + mm, k = k0 + kk;
+            As[kk][mm] = (m < M && k < K) ? load_a(A, m, k) : 0.f;
+            const int n = n0 + mm;
+            Bs[kk][mm] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kp = 0; kp < 8; ++kp) {
+            const float av = As[2 * kp + (lane >> 5)][wm * 32 + (lane & 31)];
+            const float bv = Bs[2 * kp + (lane >> 5)][wn * 32 + (lane & 31)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // C/D map (32x32, 16 regs): col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+        const int j = lane & 31;
+        const int m = m0 + wm * 32 + i, n = n0 + wn * 32 + j;
+        if (m < M && n < N) store_ep(E, m, n, acc[r]);
+    }
+}
+
+hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, const GemmEp& e,
+                       hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    dim3 grid((M + 63) / 64, (N + 63) / 64);
+    hipLaunchKernelGGL(k_gemm, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    return hipGetLastError();
+}
+
+// Stretch2d(s, 1) followed by Conv2d(1, 1, (1, 2s+1), padding (0, s)), per mel channel:
+// out(c, o) = sum_d w[d] * in_str(c, o + d - s), in_str(c, i) = in(c, i / s) for
+// 0 <= i < W_in * s, else 0; in(c, i) = src[c][i - in_pad] inside [in_pad, in_pad + T_in).
+__global__ __launch_bounds__(kThreads) void k_mel_stencil(const float* in, int in_pad, int T_in,
+                                                          int W_in, float* out, int s,
+                                                          const float* w, int out_lo,
+                                                          int out_len, int ld_out) {
+    const int oo = blockIdx.x * kThreads + threadIdx.x;
+    const int c = blockIdx.y;
+    if (oo >= out_len) return;
+    const int o = out_lo + oo;
+    const int W_out = W_in * s;
+    const float* src = in + (size_t)c * T_in;
+    float acc = 0.f;
+    for (int d = 0; d <= 2 * s; ++d) {
+        const int i = o + d - s;
+        if (i >= 0 && i < W_out) {
+            const int si = i / s - in_pad;
+            const float v = (si >= 0 && si < T_in) ? src[si] : 0.f;
+            acc = fmaf(w[d], v, acc);
+        }
+    }
+    out[(size_t)c * ld_out + oo] = acc;
+}
+
+hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, float* out,
+                              int scale, const float* w, int c, int out_lo, int out_len,
+                              int ld_out, hipStream_t s) {
+    if (out_len <= 0) return hipSuccess;
+    dim3 grid((out_len + kThreads - 1) / kThreads, c);
+    hipLaunchKernelGGL(k_mel_stencil, grid, dim3(kThreads), 0, s, in, in_pad, T_in, W_in, out,
+                       scale, w, out_lo, out_len, ld_out);
+    return hipGetLastError();
+}
+
+}  // namespace wrnn

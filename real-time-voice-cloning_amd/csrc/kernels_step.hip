@@ -1,0 +1,516 @@
+// Recurrent-step kernels of the MI355X WaveRNN vocoder.
+//
+// One autoregressive step of WaveRNN.generate (reference: vocoder/models/fatchord_version.py
+// :192-236, runtimeracer_version.py:242-291) is a chain of "stage" launches. Each stage is one
+// all-to-all seam of the recurrence: it computes a fp32 matrix-vector product for every fold
+// row (the batch) plus the elementwise layer that follows it (GRU gates, bias, ReLU), and may
+// carry extra independent segments (W_hh h for the next step, W_ih1 cI for the next step) that
+// are off the critical path. The chain is captured in HIP graphs by runtime.hip.
+//
+// Tile scheme (256 threads): a workgroup owns OT outputs of one segment for RT fold rows.
+// Its weight tile is loaded once into registers (packed so each wave reads contiguous
+// memory), the RT x K input rows are staged in LDS, every thread accumulates OPL x RT
+// partial dot products over its k-chunk (fma chain in ascending k), the partials are reduced
+// across k-chunks through LDS in a fixed order (deterministic), and the epilogue is applied by
+// the thread that owns the final (unit, row) pair.
+#include "wrnn_kernels.h"
+#include "philox.h"
+
+namespace wrnn {
+
+template <int CFG>
+struct Tile;
+template <>
+struct Tile<CFG3> {
+    static constexpr int OPL = 3, NOG = 4;
+};
+template <>
+struct Tile<CFG2> {
+    static constexpr int OPL = 2, NOG = 8;
+};
+template <>
+struct Tile<CFG1> {
+    static constexpr int OPL = 1, NOG = 4;
+};
+
+__device__ __forceinline__ int frame_of(const RowInfo& ri, int t, int hop) {
+    const int rel = ri.rel0 + t;
+    return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
+}
+
+__device__ __forceinline__ float sigmoid_ref(float x) {
+    // torch CPU sigmoid: 1 / (1 + exp(-x))
+    return 1.0f / (1.0f + expf(-x));
+}
+
+// torch GRUCell (aten/native/RNN.cpp GRUCell): r = sig(gh_r + gi_r), z = sig(gh_z + gi_z),
+// n = tanh(gi_n + gh_n * r), h' = (h - n) * z + n  -- separate roundings, no contraction.
+__device__ __forceinline__ float gru_cell(float gi_r, float gi_z, float gi_n, float gh_r,
+                                          float gh_z, float gh_n, float h) {
+#pragma clang fp contract(off)
+    const float r = sigmoid_ref(gh_r + gi_r);
+    const float z = sigmoid_ref(gh_z + gi_z);
+    const float ghr = gh_n * r;
+    const float n = tanhf(gi_n + ghr);
+    const float d = h - n;
+    const float dz = d * z;
+    return dz + n;
+}
+
+__device__ __forceinline__ float add_nc(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+
+template <int K, int RT, int CFG>
+__device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int tile, int row0,
+                                         float* lds) {
+    constexpr int OPL = Tile<CFG>::OPL, NOG = Tile<CFG>::NOG;
+    constexpr int KC = kThreads / NOG;
+    constexpr int KR = K / KC;
+    static_assert(KR % 4 == 0, "k-chunk must be a multiple of 4");
+    const int tid = threadIdx.x;
+    const int og = tid % NOG, kc = tid / NOG;
+    const int nrows = a.nrows;
+
+    // 1. weight tile -> registers; packed [tile][kc][og][j][kk] == [tile][tid][j][kk]
+    float w[OPL][KR];
+    {
+        const float4* wp = reinterpret_cast<const float4*>(
+            sg.W + ((size_t)tile * kThreads + tid) * (size_t)(OPL * KR));
+#pragma unroll
+        for (int j = 0; j < OPL; ++j)
+#pragma unroll
+            for (int q = 0; q < KR / 4; ++q) {
+                const float4 v = wp[j * (KR / 4) + q];
+                w[j][4 * q + 0] = v.x;
+                w[j][4 * q + 1] = v.y;
+                w[j][4 * q + 2] = v.z;
+                w[j][4 * q + 3] = v.w;
+            }
+    }
+
+    // 2. RT input rows -> LDS Xs[b][K] (rows past nrows are zero)
+    float4* Xs4 = reinterpret_cast<float4*>(lds);
+    for (int e = tid; e < RT * (K / 4); e += kThreads) {
+        const int b = e / (K / 4), q = e % (K / 4);
+        const int r = row0 + b;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < nrows) {
+            const float* xr = sg.X + sg.x_off + (long long)r * sg.x_ld +
+                              (long long)a.rows[r].pos0 * sg.x_pld;
+            v = reinterpret_cast<const float4*>(xr)[q];
+        }
+        Xs4[e] = v;
+    }
+    __syncthreads();
+
+    // 3. partial dot products over this thread's k-chunk
+    float acc[OPL][RT];
+#pragma unroll
+    for (int j = 0; j < OPL; ++j)
+#pragma unroll
+        for (int b = 0; b < RT; ++b) acc[j][b] = 0.f;
+#pragma unroll
+    for (int b = 0; b < RT; ++b) {
+#pragma unroll
+        for (int q = 0; q < KR / 4; ++q) {
+            const float4 xv = Xs4[b * (K / 4) + kc * (KR / 4) + q];
+#pragma unroll
+            for (int j = 0; j < OPL; ++j) {
+                float s = acc[j][b];
+                s = fmaf(w[j][4 * q + 0], xv.x, s);
+                s = fmaf(w[j][4 * q + 1], xv.y, s);
+                s = fmaf(w[j][4 * q + 2], xv.z, s);
+                s = fmaf(w[j][4 * q + 3], xv.w, s);
+                acc[j][b] = s;
+            }
+        }
+    }
+    __syncthreads();
+
+    // 4. partials -> LDS red[kc][og][j][b]
+    float* red = lds;
+#pragma unroll
+    for (int j = 0; j < OPL; ++j)
+#pragma unroll
+        for (int b = 0; b < RT; ++b) red[((kc * NOG + og) * OPL + j) * RT + b] = acc[j][b];
+    __syncthreads();
+
+    // 5. reduce over k-chunks (fixed order) and apply the epilogue
+    const int H = sg.H;
+    for (int p = tid; p < NOG * RT; p += kThreads) {
+        const int pog = p / RT, b = p % RT;
+        const int r = row0 + b;
+        if (r >= nrows) continue;
+        float s[OPL];
+#pragma unroll
+        for (int j = 0; j < OPL; ++j) {
+            float v = red[(pog * OPL + j) * RT + b];
+            for (int c = 1; c < KC; ++c) v += red[((c * NOG + pog) * OPL + j) * RT + b];
+            s[j] = v;
+        }
+        if constexpr (CFG == CFG3) {
+            const int u = tile * NOG + pog;  // unit
+            if (u * 3 >= sg.n_out) continue;
+            if (sg.kind == EPI_GRU) {
+                const float* cr =
+                    sg.cond + (size_t)frame_of(a.rows[r], a.t, a.hop) * (size_t)sg.c_ld;
+                const float gi_r = add_nc(s[0], cr[u]);
+                const float gi_z = add_nc(s[1], cr[H + u]);
+                const float gi_n = add_nc(s[2], cr[2 * H + u]);
+                const float* gh = sg.gh + (size_t)r * 3 * H;
+                const float hp = sg.h[(size_t)r * H + u];
+                const float hn = gru_cell(gi_r, gi_z, gi_n, gh[u], gh[H + u], gh[2 * H + u], hp);
+                const float* xr = sg.X + sg.x_off + (long long)r * sg.x_ld +
+                                  (long long)a.rows[r].pos0 * sg.x_pld;
+                sg.h[(size_t)r * H + u] = hn;
+                sg.xout[(size_t)r * H + u] = add_nc(xr[u], hn);
+            } else {  // EPI_BIAS3
+                float* y = sg.Y + (size_t)r * sg.y_ld;
+                y[u] = add_nc(s[0], sg.cond[u]);
+                y[H + u] = add_nc(s[1], sg.cond[H + u]);
+                y[2 * H + u] = add_nc(s[2], sg.cond[2 * H + u]);
+            }
+        } else {
+            const float* cr = sg.cond + (size_t)frame_of(a.rows[r], a.t, a.hop) * (size_t)sg.c_ld;
+            float* y = sg.Y + (size_t)r * sg.y_ld;
+#pragma unroll
+            for (int j = 0; j < OPL; ++j) {
+                const int o = (tile * NOG + pog) * OPL + j;
+                if (o < sg.n_out) {
+                    float v = add_nc(s[j], cr[o]);
+                    if (sg.kind == EPI_COND_RELU) v = v > 0.f ? v : 0.f;
+                    y[o] = v;
+                }
+            }
+        }
+    }
+}
+
+template <int K, int RT>
+__global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    uint32_t t_begin = 0;
+    if (a.stamps) t_begin = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    const int bx = blockIdx.x;
+    const int row0 = blockIdx.y * RT;
+    int s = 0;
+    while (s + 1 < a.nseg && bx >= a.tile_start[s + 1]) ++s;
+    const Seg& sg = a.seg[s];
+    const int tile = bx - a.tile_start[s];
+    switch (sg.cfg) {
+        case CFG3: seg_tile<K, RT, CFG3>(a, sg, tile, row0, lds); break;
+        case CFG2: seg_tile<K, RT, CFG2>(a, sg, tile, row0, lds); break;
+        default: seg_tile<K, RT, CFG1>(a, sg, tile, row0, lds); break;
+    }
+    if (a.stamps) {
+        __syncthreads();
+        const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+        if (threadIdx.x == 0 && wg < kMaxStampWG) {
+            a.stamps[2 * wg] = t_begin;
+            a.stamps[2 * wg + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
+template <int K, int RT>
+static size_t stage_lds_bytes() {
+    const size_t xs = (size_t)RT * K * sizeof(float);
+    const size_t red = (size_t)kThreads * 3 * RT * sizeof(float);  // max OPL = 3
+    return xs > red ? xs : red;
+}
+
+template <int K, int RT>
+static hipError_t prepare_stage_t() {
+    return hipFuncSetAttribute((const void*)k_stage<K, RT>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)stage_lds_bytes<K, RT>());
+}
+
+template <int K, int RT>
+static hipError_t launch_stage_t(const StageArgs& a, int n_row_tiles, hipStream_t s) {
+    const int n_tiles = a.tile_start[a.nseg];
+    const size_t lds = stage_lds_bytes<K, RT>();
+    hipLaunchKernelGGL((k_stage<K, RT>), dim3(n_tiles, n_row_tiles), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+#define WRNN_RT_CASES(K)                                                  \
+    switch (RT) {                                                         \
+        case 4: return launch_stage_t<K, 4>(a, n_row_tiles, s);           \
+        case 8: return launch_stage_t<K, 8>(a, n_row_tiles, s);           \
+        case 12: return launch_stage_t<K, 12>(a, n_row_tiles, s);         \
+        case 16: return launch_stage_t<K, 16>(a, n_row_tiles, s);         \
+        case 20: return launch_stage_t<K, 20>(a, n_row_tiles, s);         \
+        case 24: return launch_stage_t<K, 24>(a, n_row_tiles, s);         \
+        case 32: return launch_stage_t<K, 32>(a, n_row_tiles, s);         \
+        default: return hipErrorInvalidValue;                             \
+    }
+
+#define WRNN_RT_PREP(K)                               \
+    switch (RT) {                                     \
+        case 4: return prepare_stage_t<K, 4>();       \
+        case 8: return prepare_stage_t<K, 8>();       \
+        case 12: return prepare_stage_t<K, 12>();     \
+        case 16: return prepare_stage_t<K, 16>();     \
+        case 20: return prepare_stage_t<K, 20>();     \
+        case 24: return prepare_stage_t<K, 24>();     \
+        case 32: return prepare_stage_t<K, 32>();     \
+        default: return hipErrorInvalidValue;         \
+    }
+
+hipError_t prepare_stage(int K, int RT) {
+    if (K == 512) {
+        WRNN_RT_PREP(512)
+    } else if (K == 256) {
+        WRNN_RT_PREP(256)
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_stage(const StageArgs& a, int K, int RT, int n_row_tiles, hipStream_t s) {
+    if (K == 512) {
+        WRNN_RT_CASES(512)
+    } else if (K == 256) {
+        WRNN_RT_CASES(256)
+    }
+    return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------
+// Sampling + GRU1 of the next step (one workgroup per fold row).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float v2 = __shfl_xor(v, o, 64);
+        const int i2 = __shfl_xor(i, o, 64);
+        if (v2 > v || (v2 == v && i2 < i)) {
+            v = v2;
+            i = i2;
+        }
+    }
+}
+
+__device__ float block_max(float v, float* sh) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < kThreads / 64; ++i) r = fmaxf(r, sh[i]);
+    return r;
+}
+__device__ float block_sum(float v, float* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < kThreads / 64; ++i) r += sh[i];
+    return r;
+}
+
+constexpr int kMaxClassesPerThread = 16;  // n_classes <= 4096 (bits <= 12)
+
+__global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
+    __shared__ float shf[8];
+    __shared__ int shi[8];
+    __shared__ float xsh;
+    __shared__ uint32_t words[12];
+    const int r = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    float x = 0.f;
+    if (a.t >= 0) {
+        const int n = a.n_classes;
+        const float* lg = a.logits + (size_t)r * n;
+        if (a.mode == 0) {
+            const float* qn = a.noise + ((size_t)a.t * a.nrows + r) * n;
+            float l[kMaxClassesPerThread], q[kMaxClassesPerThread];
+            float m = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < kMaxClassesPerThread; ++i) {
+                const int k = tid + i * kThreads;
+                l[i] = k < n ? lg[k] : -INFINITY;
+                q[i] = k < n ? qn[k] : 1.f;
+                m = fmaxf(m, l[i]);
+            }
+            m = block_max(m, shf);
+            float e[kMaxClassesPerThread];
+            float se = 0.f;
+#pragma unroll
+            for (int i = 0; i < kMaxClassesPerThread; ++i) {
+                const int k = tid + i * kThreads;
+                e[i] = k < n ? expf(l[i] - m) : 0.f;
+                se += e[i];
+            }
+            se = block_sum(se, shf);
+            float sp = 0.f;
+#pragma unroll
+            for (int i = 0; i < kMaxClassesPerThread; ++i) {
+                e[i] = e[i] / se;  // softmax
+                sp += e[i];
+            }
+            sp = block_sum(sp, shf);  // Categorical re-normalisation
+            float best = -INFINITY;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < kMaxClassesPerThread; ++i) {
+                const int k = tid + i * kThreads;
+                if (k < n) {
+                    const float ratio = (e[i] / sp) / q[i];
+                    if (ratio > best || (ratio == best && k < bi)) {
+                        best = ratio;
+                        bi = k;
+                    }
+                }
+            }
+            wave_argmax(best, bi);
+            __syncthreads();
+            if (lane == 0) {
+                shf[wv] = best;
+                shi[wv] = bi;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                float bv = shf[0];
+                int bk = shi[0];
+                for (int i = 1; i < kThreads / 64; ++i)
+                    if (shf[i] > bv || (shf[i] == bv && shi[i] < bk)) {
+                        bv = shf[i];
+                        bk = shi[i];
+                    }
+                float xv;
+                {
+#pragma clang fp contract(off)
+                    xv = (2.0f * (float)bk) / (float)(n - 1) - 1.0f;
+                }
+                a.labels[(size_t)r * a.S + a.t] = (int16_t)bk;
+                a.samples[(size_t)r * a.S + a.t] = xv;
+                xsh = xv;
+            }
+        } else {
+            // MOL: vocoder/distribution.py:104-140 with the Philox draws
+            const RowInfo ri = a.rows[r];
+            if (tid < 3) {
+                const U4 o = philox4x32_10(kMolDomain | (uint32_t)tid, (uint32_t)a.t,
+                                           (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+                words[4 * tid + 0] = o.x;
+                words[4 * tid + 1] = o.y;
+                words[4 * tid + 2] = o.z;
+                words[4 * tid + 3] = o.w;
+            }
+            __syncthreads();
+            if (wv == 0) {
+                float v = -INFINITY;
+                int idx = 0x7fffffff;
+                if (lane < 10) {
+#pragma clang fp contract(off)
+                    const float u1 = mol_uniform_from_u32(words[lane]);
+                    v = lg[lane] - logf(-logf(u1));
+                    idx = lane;
+                }
+                wave_argmax(v, idx);
+                if (lane == 0) {
+#pragma clang fp contract(off)
+                    const float u2 = mol_uniform_from_u32(words[10]);
+                    const float mean = lg[10 + idx];
+                    float ls = lg[20 + idx];
+                    const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                    ls = ls < lsmin ? lsmin : ls;
+                    const float lu = logf(u2) - logf(1.0f - u2);
+                    float xv = mean + expf(ls) * lu;
+                    xv = xv < -1.f ? -1.f : xv;
+                    xv = xv > 1.f ? 1.f : xv;
+                    a.samples[(size_t)r * a.S + a.t] = xv;
+                    xsh = xv;
+                }
+            }
+        }
+        __syncthreads();
+        x = xsh;
+    }
+    if (!a.do_gru) return;
+    // GRU1 of step t+1: gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; xI = cI + w0 x ; x1 = xI + h1
+    const int H = a.H;
+    const int p = a.rows[r].pos0 + a.t + 1;
+    const float* P1 = a.P1 + (size_t)r * 3 * H;
+    const float* gh = a.gh1 + (size_t)r * 3 * H;
+    const float* cI = a.cI + (size_t)p * H;
+    for (int j = tid; j < H; j += kThreads) {
+        const float gi_r = fmaf(a.v[j], x, P1[j]);
+        const float gi_z = fmaf(a.v[H + j], x, P1[H + j]);
+        const float gi_n = fmaf(a.v[2 * H + j], x, P1[2 * H + j]);
+        const float hp = a.h1[(size_t)r * H + j];
+        const float hn = gru_cell(gi_r, gi_z, gi_n, gh[j], gh[H + j], gh[2 * H + j], hp);
+        const float xI = fmaf(a.w0[j], x, cI[j]);
+        a.h1[(size_t)r * H + j] = hn;
+        a.x1[(size_t)r * H + j] = add_nc(xI, hn);
+    }
+}
+
+hipError_t launch_sample(const SampleArgs& a, hipStream_t s) {
+    if (a.mode == 0 && a.n_classes > kMaxClassesPerThread * kThreads) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sample, dim3(a.nrows), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// RAW noise: q[t][r][k] = Exp(1) from Philox(k>>2, t, fold, stream; seed)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_noise_raw(float4* q, int S, int nrows, int ng,
+                                                        const RowInfo* rows, uint32_t k0,
+                                                        uint32_t k1) {
+    const long long gid = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const long long total = (long long)S * nrows * ng;
+    if (gid >= total) return;
+    const int g = (int)(gid % ng);
+    const long long tr = gid / ng;
+    const int r = (int)(tr % nrows);
+    const int t = (int)(tr / nrows);
+    const U4 o = philox4x32_10((uint32_t)g, (uint32_t)t, (uint32_t)rows[r].fold, rows[r].stream,
+                               k0, k1);
+    q[gid] = make_float4(exp1_from_u32(o.x), exp1_from_u32(o.y), exp1_from_u32(o.z),
+                         exp1_from_u32(o.w));
+}
+
+hipError_t launch_noise_raw(float* q, int S, int nrows, int n_classes, const RowInfo* rows,
+                            uint32_t k0, uint32_t k1, hipStream_t s) {
+    if (n_classes % 4) return hipErrorInvalidValue;
+    const int ng = n_classes / 4;
+    const long long total = (long long)S * nrows * ng;
+    const long long blocks = (total + kThreads - 1) / kThreads;
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_noise_raw, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       reinterpret_cast<float4*>(q), S, nrows, ng, rows, k0, k1);
+    return hipGetLastError();
+}
+
+__global__ void k_fill_rows(float* dst, const float* src, int n, int rows) {
+    const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= (long long)n * rows) return;
+    dst[i] = src ? src[i % n] : 0.f;
+}
+
+hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipStream_t s) {
+    const long long total = (long long)n * rows;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_rows, dim3((unsigned)((total + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, s, dst, src, n, rows);
+    return hipGetLastError();
+}
+
+}  // namespace wrnn

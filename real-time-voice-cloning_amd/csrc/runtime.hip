@@ -1,0 +1,1346 @@
+// Host runtime of the MI355X WaveRNN vocoder: weight packing, workspace, the per-step stage
+// program, HIP-graph capture of the recurrence, and the extern "C" ABI of
+// include/wavernn_mi355x.h.
+//
+// Reference behaviour restated here (paths in RuntimeRacer/Real-Time-Voice-Cloning):
+//   generate()            vocoder/models/fatchord_version.py:155-240, runtimeracer_version.py:199-295
+//   pad/upsample          fatchord_version.py:170-172, :60-85
+//   fold_with_overlap     fatchord_version.py:290-340 (never materialised: rows index positions)
+//   load_state_dict names vocoder/inference.py:35 / base.py:18-109 topologies
+//   loadWeights/melToWav  vocoder/libwavernn/<variant>/src/WaveRNNVocoder.cpp:22-47 (errors, seed)
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "philox.h"
+#include "wavernn_mi355x.h"
+#include "wrnn_kernels.h"
+
+using namespace wrnn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPC(x)                                                                             \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            return fail(WRNN_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+#define CHECK(x)                         \
+    do {                                 \
+        int rc_ = (x);                   \
+        if (rc_ != WRNN_OK) return rc_;  \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int alloc(size_t n) {
+        if (n <= bytes && p) return WRNN_OK;
+        release();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(WRNN_ERR_OOM, "hipMalloc(" + std::to_string(n) + "): " +
+                                          hipGetErrorString(e));
+        }
+        bytes = n;
+        return WRNN_OK;
+    }
+    float* f() const { return (float*)p; }
+};
+
+struct PackedSeg {
+    std::shared_ptr<DevBuf> W;
+    int cfg = 0, n_out = 0, n_tiles = 0, K = 0;
+};
+
+// one matvec segment of a stage, in terms of named per-row slots
+enum Slot {
+    SL_NONE = -1,
+    SL_X1 = 0, SL_X2, SL_X3, SL_X4,
+    SL_Y1, SL_Y2, SL_Y3, SL_Y4,
+    SL_H1, SL_H2, SL_H3, SL_H4,
+    SL_GH1, SL_GH2, SL_GH3, SL_GH4,
+    SL_P1, SL_LOG,
+    SL_CI,  // gather from per-position cI at step t+1
+    SL_COUNT
+};
+
+struct SegDesc {
+    PackedSeg w;
+    int kind;
+    int x;          // Slot
+    int y;          // Slot (EPI_BIAS3 / EPI_COND*)
+    const float* cond;  // constant device vector (c_ld == 0) ...
+    int c_ld;       // ... or -1: per-frame conditioning at column fcol of ws.fcond
+    int fcol;
+    int gh, h, xout;  // EPI_GRU slots
+};
+
+struct StageDesc {
+    std::string name;
+    int K;
+    std::vector<SegDesc> segs;
+    bool next_step_only;  // segment list index 1.. may be dropped at the last step (P1)
+};
+
+int tile_outputs(int cfg) { return cfg == CFG3 ? 4 : (cfg == CFG2 ? 16 : 4); }
+int tile_opl(int cfg) { return cfg == CFG3 ? 3 : (cfg == CFG2 ? 2 : 1); }
+int tile_nog(int cfg) { return cfg == CFG3 ? 4 : (cfg == CFG2 ? 8 : 4); }
+
+}  // namespace
+
+struct wrnn_handle {
+    wrnn_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int H = 0, F = 0, A = 0, C = 0, R = 0, n_classes = 0, feat = 0, hop = 0, n_gru = 0, KI = 0;
+    int indent = 0;
+    std::map<std::string, std::vector<int64_t>> expected;
+    std::map<std::string, std::vector<float>> host;
+    bool finalized = false;
+    uint64_t seed = 0;
+    uint32_t stream_ctr = 0;
+
+    // ---- device weights
+    std::vector<std::shared_ptr<DevBuf>> wbufs;
+    const float* Wci = nullptr;               // conv_in (C, feat*ksz)
+    const float *bn_a = nullptr, *bn_b = nullptr;  // (1 + 2*res_blocks) x C alpha / beta
+    std::vector<const float*> Wres;           // 2*res_blocks x (C, C)
+    const float *Wco = nullptr, *bco = nullptr;
+    std::vector<const float*> upk;            // up-layer kernels
+    const float *WIT = nullptr, *bI = nullptr, *w0 = nullptr, *v1 = nullptr;
+    struct AuxCond {
+        int slice;          // aux slice index (1..3)
+        const float* WT;    // (A, n_out)
+        const float* bias;  // (n_out)
+        int n_out;
+        int offset;         // column offset inside the per-frame cond row
+    };
+    std::vector<AuxCond> auxc;
+    int cond_width = 0;
+    std::map<std::string, const float*> dvec;  // constant vectors (biases)
+    std::vector<StageDesc> stages;
+
+    // ---- workspace (capacity keyed on rows/steps)
+    struct Workspace {
+        int B = 0, S = 0, Pcap = 0, Fcap = 0, Tcap = 0;
+        DevBuf slots[SL_COUNT];
+        DevBuf labels, samples, noise, cI, fcond, rows, stamps;
+        DevBuf mel_in, act0, act1, Rb, up1, up2, melup;
+        size_t mel_in_cap = 0;
+    } ws;
+    // captured recurrence chunks: (t0, len, S if last chunk else -1, rows, timing, MOL seed)
+    std::map<std::tuple<int, int, int, int, int, uint64_t>, hipGraphExec_t> graphs;
+
+    // ---- call state
+    int last_B = 0, last_S = 0, last_L0 = 0, last_T0 = 0;
+    bool timing = false;
+    std::vector<double> stage_avg_us;
+    std::vector<int> stage_launches;
+    int nrt = 1, RT = 4;
+    std::vector<RowInfo> rows_host;
+
+    ~wrnn_handle() {
+        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    float* slot(int s) const { return ws.slots[s].f(); }
+    int slot_width(int s) const {
+        switch (s) {
+            case SL_X1: case SL_X2: case SL_X3: case SL_X4:
+            case SL_H1: case SL_H2: case SL_H3: case SL_H4: return H;
+            case SL_Y1: case SL_Y2: case SL_Y3: case SL_Y4: return F;
+            case SL_GH1: case SL_GH2: case SL_GH3: case SL_GH4: case SL_P1: return 3 * H;
+            case SL_LOG: return n_classes;
+            default: return 0;
+        }
+    }
+};
+
+namespace {
+
+std::vector<int64_t> shp(std::initializer_list<int64_t> l) { return std::vector<int64_t>(l); }
+
+void build_expected(wrnn_handle* h) {
+    auto& e = h->expected;
+    const int C = h->C, R = h->R, H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    const int k = h->cfg.pad * 2 + 1;
+    e["upsample.resnet.conv_in.weight"] = shp({C, h->feat, k});
+    auto bn = [&](const std::string& p) {
+        for (const char* f : {"weight", "bias", "running_mean", "running_var"})
+            e[p + "." + f] = shp({C});
+    };
+    bn("upsample.resnet.batch_norm");
+    for (int i = 0; i < h->cfg.res_blocks; ++i) {
+        const std::string p = "upsample.resnet.layers." + std::to_string(i);
+        e[p + ".conv1.weight"] = shp({C, C, 1});
+        e[p + ".conv2.weight"] = shp({C, C, 1});
+        bn(p + ".batch_norm1");
+        bn(p + ".batch_norm2");
+    }
+    e["upsample.resnet.conv_out.weight"] = shp({R, C, 1});
+    e["upsample.resnet.conv_out.bias"] = shp({R});
+    for (int j = 0; j < h->cfg.n_upsample; ++j)
+        e["upsample.up_layers." + std::to_string(2 * j + 1) + ".weight"] =
+            shp({1, 1, 1, 2 * h->cfg.upsample_factors[j] + 1});
+    e["I.weight"] = shp({H, h->feat + A});
+    e["I.bias"] = shp({H});
+    auto gru = [&](const std::string& nm, int inp) {
+        e[nm + ".weight_ih_l0"] = shp({3 * H, inp});
+        e[nm + ".weight_hh_l0"] = shp({3 * H, H});
+        e[nm + ".bias_ih_l0"] = shp({3 * H});
+        e[nm + ".bias_hh_l0"] = shp({3 * H});
+    };
+    auto lin = [&](const std::string& nm, int inp, int out) {
+        e[nm + ".weight"] = shp({out, inp});
+        e[nm + ".bias"] = shp({out});
+    };
+    if (h->cfg.model_type == WRNN_MODEL_FATCHORD) {
+        gru("rnn1", H);
+        gru("rnn2", H + A);
+        lin("fc1", H + A, F);
+        lin("fc2", F + A, F);
+        lin("fc3", F, n);
+    } else {
+        gru("rnn1", H);
+        gru("rnn2", H);
+        gru("rnn3", H + A);
+        gru("rnn4", H);
+        lin("fc1", H + A, F);
+        lin("fc2", F, F);
+        lin("fc3", F + A, F);
+        lin("fc4", F, F);
+        lin("fc5", F, n);
+    }
+}
+
+// upload a host float vector; returns device pointer kept alive by h->wbufs
+const float* upload(wrnn_handle* h, const std::vector<float>& v, int* rc) {
+    auto b = std::make_shared<DevBuf>();
+    *rc = b->alloc(v.size() * sizeof(float));
+    if (*rc) return nullptr;
+    hipError_t e = hipMemcpy(b->p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        *rc = fail(WRNN_ERR_HIP, std::string("hipMemcpy weights: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    h->wbufs.push_back(b);
+    return b->f();
+}
+
+// Pack rows of a PyTorch (n_rows, ld) weight for the stage tile scheme of kernels_step.hip:
+// [tile][kc][og][j][kk]; CFG3 tiles are unit-interleaved (j = gate r/z/n of unit u).
+PackedSeg pack_segment(wrnn_handle* h, const std::vector<float>& W, int n_out, int ld, int col0,
+                       int K, int cfg, int Hg, int* rc) {
+    PackedSeg ps;
+    ps.cfg = cfg;
+    ps.K = K;
+    ps.n_out = n_out;
+    const int OPL = tile_opl(cfg), NOG = tile_nog(cfg);
+    const int KC = kThreads / NOG, KR = K / KC;
+    if (cfg == CFG3) {
+        ps.n_tiles = (Hg + NOG - 1) / NOG;
+    } else {
+        const int OT = OPL * NOG;
+        ps.n_tiles = (n_out + OT - 1) / OT;
+    }
+    std::vector<float> out((size_t)ps.n_tiles * kThreads * OPL * KR, 0.f);
+    size_t idx = 0;
+    for (int tile = 0; tile < ps.n_tiles; ++tile)
+        for (int tid = 0; tid < kThreads; ++tid) {
+            const int og = tid % NOG, kc = tid / NOG;
+            for (int j = 0; j < OPL; ++j)
+                for (int kk = 0; kk < KR; ++kk, ++idx) {
+                    int o;
+                    bool valid;
+                    if (cfg == CFG3) {
+                        const int u = tile * NOG + og;
+                        valid = u < Hg;
+                        o = j * Hg + u;
+                    } else {
+                        o = (tile * NOG + og) * OPL + j;
+                        valid = o < n_out;
+                    }
+                    const int k = kc * KR + kk;
+                    out[idx] = valid ? W[(size_t)o * ld + col0 + k] : 0.f;
+                }
+        }
+    auto b = std::make_shared<DevBuf>();
+    *rc = b->alloc(out.size() * sizeof(float));
+    if (*rc) return ps;
+    hipError_t e = hipMemcpy(b->p, out.data(), out.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) *rc = fail(WRNN_ERR_HIP, "hipMemcpy packed segment");
+    ps.W = b;
+    return ps;
+}
+
+std::vector<float> transpose_cols(const std::vector<float>& W, int rows, int ld, int col0,
+                                  int ncols) {
+    // returns (ncols, rows): out[k][o] = W[o][col0 + k]
+    std::vector<float> out((size_t)ncols * rows);
+    for (int k = 0; k < ncols; ++k)
+        for (int o = 0; o < rows; ++o) out[(size_t)k * rows + o] = W[(size_t)o * ld + col0 + k];
+    return out;
+}
+
+int do_finalize(wrnn_handle* h) {
+    for (auto& kv : h->expected)
+        if (!h->host.count(kv.first))
+            return fail(WRNN_ERR_INVALID, "missing state-dict tensor '" + kv.first + "'");
+    auto& T = h->host;
+    int rc = WRNN_OK;
+    const int C = h->C, H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    h->wbufs.clear();
+    h->stages.clear();
+    h->auxc.clear();
+    h->dvec.clear();
+    h->Wres.clear();
+    h->upk.clear();
+    // ---- upsample network
+    h->Wci = upload(h, T["upsample.resnet.conv_in.weight"], &rc);
+    CHECK(rc);
+    std::vector<float> alpha, beta;
+    auto push_bn = [&](const std::string& p) {
+        const auto& w = T[p + ".weight"];
+        const auto& b = T[p + ".bias"];
+        const auto& m = T[p + ".running_mean"];
+        const auto& v = T[p + ".running_var"];
+        for (int c = 0; c < C; ++c) {
+            // torch CPU eval batch_norm: invstd = 1/sqrt(var+eps); alpha = invstd*w;
+            // beta = b - mean*alpha (aten/native/cpu/batch_norm_kernel.cpp)
+            volatile float vs = v[c] + 1e-5f;
+            volatile float sq = std::sqrt((float)vs);
+            volatile float invstd = 1.0f / (float)sq;
+            volatile float al = (float)invstd * w[c];
+            volatile float mb = m[c] * (float)al;
+            alpha.push_back((float)al);
+            beta.push_back(b[c] - (float)mb);
+        }
+    };
+    push_bn("upsample.resnet.batch_norm");
+    for (int i = 0; i < h->cfg.res_blocks; ++i) {
+        const std::string p = "upsample.resnet.layers." + std::to_string(i);
+        push_bn(p + ".batch_norm1");
+        push_bn(p + ".batch_norm2");
+        h->Wres.push_back(upload(h, T[p + ".conv1.weight"], &rc));
+        CHECK(rc);
+        h->Wres.push_back(upload(h, T[p + ".conv2.weight"], &rc));
+        CHECK(rc);
+    }
+    h->bn_a = upload(h, alpha, &rc);
+    CHECK(rc);
+    h->bn_b = upload(h, beta, &rc);
+    CHECK(rc);
+    h->Wco = upload(h, T["upsample.resnet.conv_out.weight"], &rc);
+    CHECK(rc);
+    h->bco = upload(h, T["upsample.resnet.conv_out.bias"], &rc);
+    CHECK(rc);
+    for (int j = 0; j < h->cfg.n_upsample; ++j) {
+        h->upk.push_back(upload(h, T["upsample.up_layers." + std::to_string(2 * j + 1) + ".weight"], &rc));
+        CHECK(rc);
+    }
+    // ---- input layer I: x0 = [x, mel(80), a1[:A-1]] (fatchord_version.py:198-199)
+    const auto& WI = T["I.weight"];
+    const int ldI = h->feat + A;
+    h->KI = h->feat + A - 1;
+    h->WIT = upload(h, transpose_cols(WI, H, ldI, 1, h->KI), &rc);
+    CHECK(rc);
+    h->bI = upload(h, T["I.bias"], &rc);
+    CHECK(rc);
+    std::vector<float> w0(H);
+    for (int o = 0; o < H; ++o) w0[o] = WI[(size_t)o * ldI];
+    h->w0 = upload(h, w0, &rc);
+    CHECK(rc);
+    // v = W_ih1 . w0 (the rank-1 x-term of rnn1's input projection)
+    {
+        const auto& Wih1 = T["rnn1.weight_ih_l0"];
+        std::vector<float> v(3 * H);
+        for (int o = 0; o < 3 * H; ++o) {
+            double s = 0;
+            for (int k = 0; k < H; ++k) s += (double)Wih1[(size_t)o * H + k] * (double)w0[k];
+            v[o] = (float)s;
+        }
+        h->v1 = upload(h, v, &rc);
+        CHECK(rc);
+    }
+    auto dv = [&](const std::string& key) -> const float* {
+        if (!h->dvec.count(key)) {
+            h->dvec[key] = upload(h, T[key], &rc);
+        }
+        return h->dvec[key];
+    };
+    // ---- aux conditioning (per frame): W_aux^T (A, n_out) + bias
+    int off = 0;
+    auto add_aux = [&](int slice, const std::string& wname, const std::string& bname, int rows,
+                       int ld, int col0) {
+        wrnn_handle::AuxCond ac;
+        ac.slice = slice;
+        ac.n_out = rows;
+        ac.offset = off;
+        ac.WT = upload(h, transpose_cols(T[wname], rows, ld, col0, A), &rc);
+        ac.bias = dv(bname);
+        off += rows;
+        h->auxc.push_back(ac);
+        return ac.offset;
+    };
+    const int K = H;  // recurrent inner dimension
+    if (H != F) return fail(WRNN_ERR_INVALID, "rnn_dims != fc_dims is not supported");
+    if (K != 256 && K != 512)
+        return fail(WRNN_ERR_INVALID, "rnn_dims must be 256 or 512 (got " + std::to_string(K) + ")");
+    if (n % 4) return fail(WRNN_ERR_INVALID, "n_classes must be a multiple of 4");
+    auto seg_gru = [&](const std::string& gname, int col0_ld, int x, int gh, int hh, int xout,
+                       const float* cond, int fc) {
+        SegDesc s{};
+        s.w = pack_segment(h, T[gname + ".weight_ih_l0"], 3 * H, col0_ld, 0, K, CFG3, H, &rc);
+        s.kind = EPI_GRU;
+        s.x = x;
+        s.y = SL_NONE;
+        s.cond = cond;
+        s.c_ld = fc >= 0 ? -1 : 0;
+        s.fcol = fc;
+        s.gh = gh;
+        s.h = hh;
+        s.xout = xout;
+        return s;
+    };
+    auto seg_hh = [&](const std::string& gname, int hsl, int ghsl) {
+        SegDesc s{};
+        s.w = pack_segment(h, T[gname + ".weight_hh_l0"], 3 * H, H, 0, K, CFG3, H, &rc);
+        s.kind = EPI_BIAS3;
+        s.x = hsl;
+        s.y = ghsl;
+        s.cond = dv(gname + ".bias_hh_l0");
+        s.c_ld = 0;
+        s.fcol = -1;
+        s.gh = s.h = s.xout = SL_NONE;
+        return s;
+    };
+    auto seg_p1 = [&]() {
+        SegDesc s{};
+        s.w = pack_segment(h, T["rnn1.weight_ih_l0"], 3 * H, H, 0, K, CFG3, H, &rc);
+        s.kind = EPI_BIAS3;
+        s.x = SL_CI;
+        s.y = SL_P1;
+        s.cond = dv("rnn1.bias_ih_l0");
+        s.c_ld = 0;
+        s.fcol = -1;
+        s.gh = s.h = s.xout = SL_NONE;
+        return s;
+    };
+    auto seg_fc = [&](const std::string& nm, int n_out, int ld, int x, int y, bool relu,
+                      const float* cond, int fc) {
+        SegDesc s{};
+        s.w = pack_segment(h, T[nm + ".weight"], n_out, ld, 0, K, CFG1, 0, &rc);
+        s.kind = relu ? EPI_COND_RELU : EPI_COND;
+        s.x = x;
+        s.y = y;
+        s.cond = cond;
+        s.c_ld = fc >= 0 ? -1 : 0;
+        s.fcol = fc;
+        s.gh = s.h = s.xout = SL_NONE;
+        return s;
+    };
+    auto fcol = [](int offset) { return offset; };
+    if (h->cfg.model_type == WRNN_MODEL_FATCHORD) {
+        const int oG2 = add_aux(1, "rnn2.weight_ih_l0", "rnn2.bias_ih_l0", 3 * H, H + A, H);
+        const int oF1 = add_aux(2, "fc1.weight", "fc1.bias", F, H + A, H);
+        const int oF2 = add_aux(3, "fc2.weight", "fc2.bias", F, F + A, F);
+        CHECK(rc);
+        h->cond_width = off;
+        StageDesc s0{"gru2", K, {}, false};
+        s0.segs.push_back(seg_gru("rnn2", H + A, SL_X1, SL_GH2, SL_H2, SL_X2, nullptr, fcol(oG2)));
+        s0.segs.push_back(seg_hh("rnn1", SL_H1, SL_GH1));
+        StageDesc s1{"fc1", K, {}, false};
+        s1.segs.push_back(seg_fc("fc1", F, H + A, SL_X2, SL_Y1, true, nullptr, fcol(oF1)));
+        s1.segs.push_back(seg_hh("rnn2", SL_H2, SL_GH2));
+        StageDesc s2{"fc2", K, {}, true};
+        s2.segs.push_back(seg_fc("fc2", F, F + A, SL_Y1, SL_Y2, true, nullptr, fcol(oF2)));
+        s2.segs.push_back(seg_p1());
+        StageDesc s3{"fc3", K, {}, false};
+        s3.segs.push_back(seg_fc("fc3", n, F, SL_Y2, SL_LOG, false, dv("fc3.bias"), -1));
+        CHECK(rc);
+        h->stages = {s0, s1, s2, s3};
+    } else {
+        const int oG3 = add_aux(1, "rnn3.weight_ih_l0", "rnn3.bias_ih_l0", 3 * H, H + A, H);
+        const int oF1 = add_aux(2, "fc1.weight", "fc1.bias", F, H + A, H);
+        const int oF3 = add_aux(3, "fc3.weight", "fc3.bias", F, F + A, F);
+        CHECK(rc);
+        h->cond_width = off;
+        StageDesc s0{"gru2", K, {}, false};
+        s0.segs.push_back(seg_gru("rnn2", H, SL_X1, SL_GH2, SL_H2, SL_X2, dv("rnn2.bias_ih_l0"), -1));
+        s0.segs.push_back(seg_hh("rnn1", SL_H1, SL_GH1));
+        StageDesc s1{"gru3", K, {}, false};
+        s1.segs.push_back(seg_gru("rnn3", H + A, SL_X2, SL_GH3, SL_H3, SL_X3, nullptr, fcol(oG3)));
+        s1.segs.push_back(seg_hh("rnn2", SL_H2, SL_GH2));
+        StageDesc s2{"gru4", K, {}, false};
+        s2.segs.push_back(seg_gru("rnn4", H, SL_X3, SL_GH4, SL_H4, SL_X4, dv("rnn4.bias_ih_l0"), -1));
+        s2.segs.push_back(seg_hh("rnn3", SL_H3, SL_GH3));
+        StageDesc s3{"fc1", K, {}, false};
+        s3.segs.push_back(seg_fc("fc1", F, H + A, SL_X4, SL_Y1, false, nullptr, fcol(oF1)));
+        s3.segs.push_back(seg_hh("rnn4", SL_H4, SL_GH4));
+        StageDesc s4{"fc2", K, {}, true};
+        s4.segs.push_back(seg_fc("fc2", F, F, SL_Y1, SL_Y2, true, dv("fc2.bias"), -1));
+        s4.segs.push_back(seg_p1());
+        StageDesc s5{"fc3", K, {}, false};
+        s5.segs.push_back(seg_fc("fc3", F, F + A, SL_Y2, SL_Y3, false, nullptr, fcol(oF3)));
+        StageDesc s6{"fc4", K, {}, false};
+        s6.segs.push_back(seg_fc("fc4", F, F, SL_Y3, SL_Y4, true, dv("fc4.bias"), -1));
+        StageDesc s7{"fc5", K, {}, false};
+        s7.segs.push_back(seg_fc("fc5", n, F, SL_Y4, SL_LOG, false, dv("fc5.bias"), -1));
+        CHECK(rc);
+        h->stages = {s0, s1, s2, s3, s4, s5, s6, s7};
+    }
+    CHECK(rc);
+    // per-frame cond pointers: mark with c_ld = -1 -> resolved against ws.fcond at launch
+    h->finalized = true;
+    for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+    h->graphs.clear();
+    return WRNN_OK;
+}
+
+int pick_rt(int B, int* nrt) {
+    static const int opts[] = {4, 8, 12, 16, 20, 24, 32};
+    if (B <= 32) {
+        for (int o : opts)
+            if (o >= B) {
+                *nrt = 1;
+                return o;
+            }
+    }
+    int best = 32, bw = 1 << 30;
+    for (int o : {16, 20, 24, 32}) {
+        const int t = (B + o - 1) / o;
+        const int w = t * o - B;
+        if (w < bw || (w == bw && o > best)) {
+            bw = w;
+            best = o;
+        }
+    }
+    *nrt = (B + best - 1) / best;
+    return best;
+}
+
+int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tmax) {
+    auto& ws = h->ws;
+    const bool grow = B > ws.B || S > ws.S || Pneed > ws.Pcap || Fneed > ws.Fcap || Tmax > ws.Tcap;
+    if (!grow) return WRNN_OK;
+    for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+    h->graphs.clear();
+    const int nB = std::max(B, ws.B), nS = std::max(S, ws.S);
+    const int nP = std::max(Pneed, ws.Pcap), nF = std::max(Fneed, ws.Fcap), nT = std::max(Tmax, ws.Tcap);
+    for (int s = 0; s < SL_CI; ++s) {
+        const int w = h->slot_width(s);
+        if (w == 0) continue;
+        ws.slots[s].release();
+        CHECK(ws.slots[s].alloc((size_t)nB * w * sizeof(float)));
+    }
+    ws.labels.release();
+    ws.samples.release();
+    ws.noise.release();
+    ws.cI.release();
+    ws.fcond.release();
+    ws.rows.release();
+    CHECK(ws.labels.alloc((size_t)nB * nS * sizeof(int16_t)));
+    CHECK(ws.samples.alloc((size_t)nB * nS * sizeof(float)));
+    if (h->cfg.mode == WRNN_MODE_RAW)
+        CHECK(ws.noise.alloc((size_t)nS * nB * h->n_classes * sizeof(float)));
+    CHECK(ws.cI.alloc((size_t)nP * h->H * sizeof(float)));
+    CHECK(ws.fcond.alloc((size_t)nF * h->cond_width * sizeof(float)));
+    CHECK(ws.rows.alloc((size_t)nB * sizeof(RowInfo)));
+    // upsample scratch for one utterance of <= nT frames
+    const int tot = h->hop;  // product of factors
+    ws.act0.release();
+    ws.act1.release();
+    ws.Rb.release();
+    ws.up1.release();
+    ws.up2.release();
+    ws.melup.release();
+    CHECK(ws.act0.alloc((size_t)h->C * nT * sizeof(float)));
+    CHECK(ws.act1.alloc((size_t)h->C * nT * sizeof(float)));
+    CHECK(ws.Rb.alloc((size_t)h->R * nT * sizeof(float)));
+    size_t w1 = (size_t)(nT + 2 * h->cfg.pad) * h->cfg.upsample_factors[0];
+    size_t w2 = w1 * (h->cfg.n_upsample > 1 ? h->cfg.upsample_factors[1] : 1);
+    CHECK(ws.up1.alloc((size_t)h->feat * w1 * sizeof(float)));
+    CHECK(ws.up2.alloc((size_t)h->feat * w2 * sizeof(float)));
+    CHECK(ws.melup.alloc((size_t)h->feat * nT * tot * sizeof(float)));
+    ws.B = nB;
+    ws.S = nS;
+    ws.Pcap = nP;
+    ws.Fcap = nF;
+    ws.Tcap = nT;
+    return WRNN_OK;
+}
+
+// ---- upsample network + conditioning for one utterance --------------------------------
+int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Lpad, int pbase, int fbase) {
+    auto& ws = h->ws;
+    hipStream_t st = h->stream;
+    const int C = h->C, R = h->R, H = h->H;
+    const int ksz = 2 * h->cfg.pad + 1;
+    const int L = T * h->hop;
+    // MelResNet: conv_in (k = 2*pad+1, no padding) on the mel padded by `pad` frames
+    GemmA a{};
+    GemmB b{};
+    GemmEp e{};
+    a.kind = 0;
+    a.p = h->Wci;
+    a.ld = h->feat * ksz;
+    b.kind = 1;
+    b.p = d_mel;
+    b.T = T;
+    b.pad = 0;  // im2col index n + kk over the padded mel: padded(i) = mel(i - pad)
+    b.ksz = ksz;
+    // out frame n uses padded[n + kk] = mel[n + kk - pad]
+    b.pad = h->cfg.pad;
+    e.kind = 2;
+    e.D = ws.act0.f();
+    e.ld = T;
+    e.alpha = h->bn_a;
+    e.beta = h->bn_b;
+    e.relu = 1;
+    e.res = nullptr;
+    HIPC(launch_gemm(C, T, h->feat * ksz, a, b, e, st));
+    for (int i = 0; i < h->cfg.res_blocks; ++i) {
+        GemmA a1{};
+        GemmB b1{};
+        GemmEp e1{};
+        a1.kind = 0;
+        a1.p = h->Wres[2 * i];
+        a1.ld = C;
+        b1.kind = 0;
+        b1.p = ws.act0.f();
+        b1.ld = T;
+        e1.kind = 2;
+        e1.D = ws.act1.f();
+        e1.ld = T;
+        e1.alpha = h->bn_a + (size_t)(1 + 2 * i) * C;
+        e1.beta = h->bn_b + (size_t)(1 + 2 * i) * C;
+        e1.relu = 1;
+        HIPC(launch_gemm(C, T, C, a1, b1, e1, st));
+        GemmA a2{};
+        GemmB b2{};
+        GemmEp e2{};
+        a2.kind = 0;
+        a2.p = h->Wres[2 * i + 1];
+        a2.ld = C;
+        b2.kind = 0;
+        b2.p = ws.act1.f();
+        b2.ld = T;
+        e2.kind = 2;
+        e2.D = ws.act0.f();
+        e2.ld = T;
+        e2.alpha = h->bn_a + (size_t)(2 + 2 * i) * C;
+        e2.beta = h->bn_b + (size_t)(2 + 2 * i) * C;
+        e2.relu = 0;
+        e2.res = ws.act0.f();
+        HIPC(launch_gemm(C, T, C, a2, b2, e2, st));
+    }
+    {
+        GemmA a3{};
+        GemmB b3{};
+        GemmEp e3{};
+        a3.kind = 0;
+        a3.p = h->Wco;
+        a3.ld = C;
+        b3.kind = 0;
+        b3.p = ws.act0.f();
+        b3.ld = T;
+        e3.kind = 1;
+        e3.D = ws.Rb.f();
+        e3.ld = T;
+        e3.bias = h->bco;
+        HIPC(launch_gemm(R, T, C, a3, b3, e3, st));
+    }
+    // mel stretch+conv stencils (fatchord_version.py:68-76,83-84)
+    {
+        const int nu = h->cfg.n_upsample;
+        const float* src = d_mel;
+        int in_pad = h->cfg.pad, T_in = T, W_in = T + 2 * h->cfg.pad;
+        float* bufs[2] = {ws.up1.f(), ws.up2.f()};
+        for (int j = 0; j < nu; ++j) {
+            const int s = h->cfg.upsample_factors[j];
+            const int W_out = W_in * s;
+            const bool last = j == nu - 1;
+            float* dst = last ? ws.melup.f() : bufs[j & 1];
+            const int lo = last ? h->indent : 0;
+            const int len = last ? W_out - 2 * h->indent : W_out;
+            if (last && len != L) return fail(WRNN_ERR_INVALID, "upsample length mismatch");
+            HIPC(launch_mel_stencil(src, in_pad, T_in, W_in, dst, s, h->upk[j], h->feat, lo, len,
+                                    len, st));
+            src = dst;
+            in_pad = 0;
+            T_in = W_out;
+            W_in = W_out;
+        }
+    }
+    // cI[p] = I.weight[:,1:] . [mel_up(p), aux(p)[:A-1]] + I.bias for p in [0, Lpad)
+    {
+        GemmA a4{};
+        GemmB b4{};
+        GemmEp e4{};
+        a4.kind = 1;
+        a4.mel = ws.melup.f();
+        a4.ldm = L;
+        a4.n_mel = h->feat;
+        a4.L = L;
+        a4.hop = h->hop;
+        a4.R = ws.Rb.f();
+        a4.ldr = T;
+        a4.r_off = 0;
+        a4.n_aux = h->A - 1;
+        b4.kind = 0;
+        b4.p = h->WIT;
+        b4.ld = H;
+        e4.kind = 0;
+        e4.D = ws.cI.f() + (size_t)pbase * H;
+        e4.ld = H;
+        e4.bias = h->bI;
+        HIPC(launch_gemm(Lpad, H, h->KI, a4, b4, e4, st));
+    }
+    // per-frame aux conditioning, slot 0 = zero frame
+    for (const auto& ac : h->auxc) {
+        GemmA a5{};
+        GemmB b5{};
+        GemmEp e5{};
+        a5.kind = 2;
+        a5.R = ws.Rb.f();
+        a5.ldr = T;
+        a5.r_off = ac.slice * h->A;
+        b5.kind = 0;
+        b5.p = ac.WT;
+        b5.ld = ac.n_out;
+        e5.kind = 0;
+        e5.D = ws.fcond.f() + (size_t)fbase * h->cond_width + ac.offset;
+        e5.ld = h->cond_width;
+        e5.bias = ac.bias;
+        HIPC(launch_gemm(T + 1, ac.n_out, h->A, a5, b5, e5, st));
+    }
+    return WRNN_OK;
+}
+
+// Build the StageArgs of stage `si` at step t.
+int build_stage_args(wrnn_handle* h, int si, int t, int S, bool timing, StageArgs* out, int* K) {
+    const StageDesc& sd = h->stages[si];
+    auto& ws = h->ws;
+    StageArgs a{};
+    a.nrows = h->last_B;
+    a.t = t;
+    a.hop = h->hop;
+    a.rows = (const RowInfo*)ws.rows.p;
+    a.stamps = nullptr;
+    if (timing && t >= 0 && t % kStampEvery == 0)
+        a.stamps = (uint32_t*)ws.stamps.p +
+                   ((size_t)(t / kStampEvery) * h->stages.size() + si) * kMaxStampWG * 2;
+    int ns = 0, tile = 0;
+    for (size_t k = 0; k < sd.segs.size(); ++k) {
+        const SegDesc& d = sd.segs[k];
+        if (d.x == SL_CI && t + 1 >= S) continue;  // no next step
+        Seg& g = a.seg[ns];
+        g.W = d.w.W->f();
+        g.n_out = d.w.n_out;
+        g.n_tiles = d.w.n_tiles;
+        g.kind = d.kind;
+        g.cfg = d.w.cfg;
+        g.H = h->H;
+        if (d.x == SL_CI) {
+            g.X = ws.cI.f();
+            g.x_off = (long long)(t + 1) * h->H;
+            g.x_ld = 0;
+            g.x_pld = h->H;
+        } else {
+            g.X = h->slot(d.x);
+            g.x_off = 0;
+            g.x_ld = h->slot_width(d.x);
+            g.x_pld = 0;
+        }
+        g.Y = d.y >= 0 ? h->slot(d.y) : nullptr;
+        g.y_ld = d.y >= 0 ? h->slot_width(d.y) : 0;
+        if (d.c_ld < 0) {  // per-frame conditioning column offset
+            g.cond = ws.fcond.f() + d.fcol;
+            g.c_ld = h->cond_width;
+        } else {
+            g.cond = d.cond;
+            g.c_ld = 0;
+        }
+        g.gh = d.gh >= 0 ? h->slot(d.gh) : nullptr;
+        g.h = d.h >= 0 ? h->slot(d.h) : nullptr;
+        g.xout = d.xout >= 0 ? h->slot(d.xout) : nullptr;
+        a.tile_start[ns] = tile;
+        tile += g.n_tiles;
+        ++ns;
+    }
+    a.nseg = ns;
+    a.tile_start[ns] = tile;
+    *out = a;
+    *K = sd.K;
+    return WRNN_OK;
+}
+
+int launch_step(wrnn_handle* h, int t, int S, bool timing) {
+    hipStream_t st = h->stream;
+    for (size_t si = 0; si < h->stages.size(); ++si) {
+        StageArgs a;
+        int K;
+        CHECK(build_stage_args(h, (int)si, t, S, timing, &a, &K));
+        HIPC(launch_stage(a, K, h->RT, h->nrt, st));
+    }
+    SampleArgs sa{};
+    sa.t = t;
+    sa.S = h->ws.S;  // row stride of labels/samples = capacity
+    sa.nrows = h->last_B;
+    sa.n_classes = h->n_classes;
+    sa.mode = h->cfg.mode;
+    sa.H = h->H;
+    sa.logits = h->slot(SL_LOG);
+    sa.noise = h->ws.noise.f();
+    sa.samples = h->ws.samples.f();
+    sa.labels = (int16_t*)h->ws.labels.p;
+    sa.do_gru = t + 1 < S;
+    sa.P1 = h->slot(SL_P1);
+    sa.v = h->v1;
+    sa.gh1 = h->slot(SL_GH1);
+    sa.h1 = h->slot(SL_H1);
+    sa.x1 = h->slot(SL_X1);
+    sa.cI = h->ws.cI.f();
+    sa.w0 = h->w0;
+    sa.rows = (const RowInfo*)h->ws.rows.p;
+    sa.k0 = (uint32_t)(h->seed & 0xffffffffu);
+    sa.k1 = (uint32_t)(h->seed >> 32);
+    HIPC(launch_sample(sa, st));
+    return WRNN_OK;
+}
+
+// A noise-seed-dependent kernel argument (MOL Philox key) is baked into captured graphs, so the
+// cache key includes it through `timing` only when RAW; MOL graphs are keyed by seed below.
+int run_chunk(wrnn_handle* h, int t0, int len, int S) {
+    const bool last = t0 + len >= S;
+    const int key_S = last ? S : -1;
+    auto key = std::make_tuple(t0, len, key_S, h->last_B, h->timing ? 1 : 0,
+                               h->cfg.mode == WRNN_MODE_MOL ? h->seed : (uint64_t)0);
+    auto it = h->graphs.find(key);
+    if (it == h->graphs.end()) {
+        hipGraph_t g;
+        HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        int rc = WRNN_OK;
+        for (int t = t0; t < t0 + len && rc == WRNN_OK; ++t) rc = launch_step(h, t, S, h->timing);
+        hipError_t e = hipStreamEndCapture(h->stream, &g);
+        if (rc != WRNN_OK) return rc;
+        HIPC(e);
+        hipGraphExec_t ge;
+        hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIPC(ei);
+        it = h->graphs.emplace(key, ge).first;
+    }
+    HIPC(hipGraphLaunch(it->second, h->stream));
+    return WRNN_OK;
+}
+
+void fold_shape(int L, int batched, int target, int overlap, int* B, int* S) {
+    if (!batched) {
+        *B = 1;
+        *S = L;
+        return;
+    }
+    int nf = (L - overlap) / (target + overlap);
+    const int ext = nf * (overlap + target) + overlap;
+    if (L - ext != 0) nf += 1;
+    *B = nf;
+    *S = target + 2 * overlap;
+}
+
+struct UttPlan {
+    int T, L, B, Lpad, pbase, fbase, row0;
+};
+
+int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
+                  int batched, int target, int overlap, int* row_offset, int* seq_len,
+                  wrnn_progress_fn cb, void* user) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (!h->finalized)
+        return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
+    if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
+    if (batched && (target <= 0 || overlap < 0))
+        return fail(WRNN_ERR_INVALID, "target must be > 0 and overlap >= 0");
+    if (!batched && n_utts != 1)
+        return fail(WRNN_ERR_INVALID, "unbatched generation takes one utterance");
+    std::vector<UttPlan> plan(n_utts);
+    int B = 0, S = 0, P = 0, Fr = 0, Tmax = 0;
+    for (int u = 0; u < n_utts; ++u) {
+        UttPlan& p = plan[u];
+        p.T = n_frames[u];
+        if (p.T <= 0) return fail(WRNN_ERR_INVALID, "mel has no frames");
+        p.L = p.T * h->hop;
+        int b, s;
+        fold_shape(p.L, batched, target, overlap, &b, &s);
+        if (b <= 0) return fail(WRNN_ERR_INVALID, "mel too short for target/overlap");
+        if (u && s != S) return fail(WRNN_ERR_INVALID, "inconsistent seq_len");
+        S = s;
+        p.B = b;
+        p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
+        p.pbase = P;
+        p.fbase = Fr;
+        p.row0 = B;
+        B += b;
+        P += p.Lpad;
+        Fr += p.T + 1;
+        Tmax = std::max(Tmax, p.T);
+    }
+    if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
+    CHECK(ensure_workspace(h, B, S, P, Fr, Tmax));
+    auto& ws = h->ws;
+    h->last_B = B;
+    h->last_S = S;
+    h->last_T0 = plan[0].T;
+    h->last_L0 = plan[0].L;
+    h->RT = pick_rt(B, &h->nrt);
+    // rows
+    std::vector<RowInfo> rows(B);
+    for (int u = 0; u < n_utts; ++u) {
+        const UttPlan& p = plan[u];
+        for (int f = 0; f < p.B; ++f) {
+            RowInfo& ri = rows[p.row0 + f];
+            ri.rel0 = batched ? f * (target + overlap) : 0;
+            ri.pos0 = p.pbase + ri.rel0;
+            ri.L = p.L;
+            ri.fbase = p.fbase;
+            ri.fold = f;
+            ri.stream = h->stream_ctr + (uint32_t)u;
+        }
+        if (row_offset) row_offset[u] = p.row0;
+    }
+    if (row_offset) row_offset[n_utts] = B;
+    h->rows_host = rows;
+    HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
+                        hipMemcpyHostToDevice, h->stream));
+    // upsample + conditioning per utterance
+    for (int u = 0; u < n_utts; ++u)
+        CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].Lpad, plan[u].pbase, plan[u].fbase));
+    // noise
+    if (h->cfg.mode == WRNN_MODE_RAW)
+        HIPC(launch_noise_raw(ws.noise.f(), S, B, h->n_classes, (const RowInfo*)ws.rows.p,
+                              (uint32_t)(h->seed & 0xffffffffu), (uint32_t)(h->seed >> 32),
+                              h->stream));
+    HIPC(prepare_stage(h->stages[0].K, h->RT));
+    // initial state: h = 0, gh = b_hh, then P1(0) and GRU1 of step 0
+    const int ngru = h->n_gru;
+    for (int g = 0; g < ngru; ++g) {
+        HIPC(launch_fill_rows(h->slot(SL_H1 + g), nullptr, h->H, B, h->stream));
+        HIPC(launch_fill_rows(h->slot(SL_GH1 + g), h->dvec["rnn" + std::to_string(g + 1) + ".bias_hh_l0"],
+                              3 * h->H, B, h->stream));
+    }
+    {
+        // P1 for step 0: the stage holding the SL_CI segment, run with t = -1 (x_off = 0)
+        for (size_t si = 0; si < h->stages.size(); ++si) {
+            const StageDesc& sd = h->stages[si];
+            for (const SegDesc& d : sd.segs)
+                if (d.x == SL_CI) {
+                    StageArgs a{};
+                    int K;
+                    CHECK(build_stage_args(h, (int)si, -1, S, false, &a, &K));
+                    // keep only the SL_CI segment
+                    for (int k = 0; k < a.nseg; ++k)
+                        if (a.seg[k].X == ws.cI.f()) {
+                            StageArgs b = a;
+                            b.seg[0] = a.seg[k];
+                            b.nseg = 1;
+                            b.tile_start[0] = 0;
+                            b.tile_start[1] = a.seg[k].n_tiles;
+                            HIPC(launch_stage(b, K, h->RT, h->nrt, h->stream));
+                        }
+                }
+        }
+        SampleArgs sa{};
+        sa.t = -1;
+        sa.S = ws.S;
+        sa.nrows = B;
+        sa.n_classes = h->n_classes;
+        sa.mode = h->cfg.mode;
+        sa.H = h->H;
+        sa.do_gru = 1;
+        sa.P1 = h->slot(SL_P1);
+        sa.v = h->v1;
+        sa.gh1 = h->slot(SL_GH1);
+        sa.h1 = h->slot(SL_H1);
+        sa.x1 = h->slot(SL_X1);
+        sa.cI = ws.cI.f();
+        sa.w0 = h->w0;
+        sa.rows = (const RowInfo*)ws.rows.p;
+        HIPC(launch_sample(sa, h->stream));
+    }
+    HIPC(prepare_stage(h->stages[0].K, h->RT));
+    if (h->timing) {
+        const size_t need = ((size_t)S / kStampEvery + 1) * h->stages.size() * kMaxStampWG * 2 *
+                            sizeof(uint32_t);
+        if (need > ws.stamps.bytes) {
+            for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+            h->graphs.clear();
+            ws.stamps.release();
+            CHECK(ws.stamps.alloc(need));
+        }
+        HIPC(hipMemsetAsync(ws.stamps.p, 0, need, h->stream));
+    }
+    // the recurrence, 100 steps per graph (progress granularity of the reference)
+    const int G = 100;
+    const auto t_start = std::chrono::steady_clock::now();
+    std::vector<hipEvent_t> evs;
+    int rc = WRNN_OK;
+    const int nchunks = (S + G - 1) / G;
+    evs.resize(nchunks, nullptr);
+    for (int c = 0; c < nchunks && rc == WRNN_OK; ++c) {
+        const int t0 = c * G, len = std::min(G, S - t0);
+        rc = run_chunk(h, t0, len, S);
+        if (rc) break;
+        if (cb) {
+            if (hipEventCreateWithFlags(&evs[c], hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(evs[c], h->stream) != hipSuccess) {
+                rc = fail(WRNN_ERR_HIP, "event record");
+                break;
+            }
+            // report the previous chunk once it is done (keeps one chunk queued ahead)
+            if (c >= 1) {
+                (void)hipEventSynchronize(evs[c - 1]);
+                const int i = (c - 1) * G;
+                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+                const double rate = (i + 1) / std::max(el, 1e-9) * B / 1000.0;
+                if (cb(user, i, S, B, rate)) rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+            }
+        }
+    }
+    if (rc == WRNN_OK && cb && nchunks >= 1) {
+        (void)hipEventSynchronize(evs[nchunks - 1]);
+        const int i = (nchunks - 1) * G;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        if (cb(user, i, S, B, (i + 1) / std::max(el, 1e-9) * B / 1000.0))
+            rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+    }
+    for (auto e : evs)
+        if (e) (void)hipEventDestroy(e);
+    if (rc) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    if (seq_len) *seq_len = S;
+    h->stream_ctr += (uint32_t)n_utts;
+    return WRNN_OK;
+}
+
+int collect_timing(wrnn_handle* h) {
+    const int ns = (int)h->stages.size();
+    h->stage_avg_us.assign(ns, 0.0);
+    h->stage_launches.assign(ns, 0);
+    if (!h->timing) return WRNN_OK;
+    const int S = h->last_S;
+    const int nt = (S - 1) / kStampEvery + 1;
+    std::vector<uint32_t> st((size_t)nt * ns * kMaxStampWG * 2);
+    HIPC(hipStreamSynchronize(h->stream));
+    HIPC(hipMemcpy(st.data(), h->ws.stamps.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int i = 0; i < nt; ++i) {
+        const int t = i * kStampEvery;
+        for (int s = 0; s < ns; ++s) {
+            StageArgs a;
+            int K;
+            if (build_stage_args(h, s, t, S, false, &a, &K)) continue;
+            const int nwg = std::min(kMaxStampWG, a.tile_start[a.nseg] * h->nrt);
+            const uint32_t* p = st.data() + ((size_t)i * ns + s) * kMaxStampWG * 2;
+            bool ok = true;
+            long long lo = 0, hi = 0;
+            const uint32_t ref = p[0];
+            for (int w = 0; w < nwg && ok; ++w) {
+                if (p[2 * w] == 0 && p[2 * w + 1] == 0) ok = false;
+                const long long b = (int32_t)(p[2 * w] - ref), e = (int32_t)(p[2 * w + 1] - ref);
+                lo = w ? std::min(lo, b) : b;
+                hi = w ? std::max(hi, e) : e;
+            }
+            if (!ok || hi <= lo) continue;
+            h->stage_avg_us[s] += (double)(hi - lo) * 0.01;  // 100 MHz ticks -> us
+            h->stage_launches[s] += 1;
+        }
+    }
+    for (int s = 0; s < ns; ++s)
+        if (h->stage_launches[s]) h->stage_avg_us[s] /= h->stage_launches[s];
+    return WRNN_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+// extern "C" ABI
+// =========================================================================================
+extern "C" {
+
+const char* wrnn_version(void) { return "wavernn-mi355x 0.1 (gfx950)"; }
+
+const char* wrnn_last_error(void) { return g_err.c_str(); }
+
+int wrnn_device_count(int* count) {
+    if (!count) return fail(WRNN_ERR_INVALID, "null count");
+    HIPC(hipGetDeviceCount(count));
+    return WRNN_OK;
+}
+
+int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
+    if (!cfg || !out) return fail(WRNN_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->model_type != WRNN_MODEL_FATCHORD && cfg->model_type != WRNN_MODEL_RUNTIMERACER)
+        return fail(WRNN_ERR_INVALID, "Invalid model type " + std::to_string(cfg->model_type));
+    if (cfg->mode != WRNN_MODE_RAW && cfg->mode != WRNN_MODE_MOL)
+        return fail(WRNN_ERR_INVALID, "Unknown model mode value - " + std::to_string(cfg->mode));
+    if (cfg->mode == WRNN_MODE_RAW && (cfg->bits < 2 || cfg->bits > 12))
+        return fail(WRNN_ERR_INVALID, "bits must be in [2, 12]");
+    if (cfg->n_upsample < 1 || cfg->n_upsample > 4)
+        return fail(WRNN_ERR_INVALID, "n_upsample must be in [1, 4]");
+    int prod = 1;
+    for (int i = 0; i < cfg->n_upsample; ++i) prod *= cfg->upsample_factors[i];
+    if (prod != cfg->hop_length)
+        return fail(WRNN_ERR_INVALID, "prod(upsample_factors) != hop_length");  // base.py:27
+    if (cfg->res_out_dims % 4 || cfg->res_out_dims / 4 < 2)
+        return fail(WRNN_ERR_INVALID, "res_out_dims must be a multiple of 4");
+    std::unique_ptr<wrnn_handle> h(new wrnn_handle());
+    h->cfg = *cfg;
+    h->device = device;
+    h->H = cfg->rnn_dims;
+    h->F = cfg->fc_dims;
+    h->A = cfg->res_out_dims / 4;
+    h->C = cfg->compute_dims;
+    h->R = cfg->res_out_dims;
+    h->feat = cfg->feat_dims;
+    h->hop = cfg->hop_length;
+    h->n_classes = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : 30;
+    h->n_gru = cfg->model_type == WRNN_MODEL_FATCHORD ? 2 : 4;
+    h->indent = cfg->pad * prod;
+    build_expected(h.get());
+    HIPC(hipSetDevice(device));
+    HIPC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    *out = h.release();
+    return WRNN_OK;
+}
+
+void wrnn_destroy(wrnn_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    delete h;
+}
+
+int wrnn_load_tensor(wrnn_handle* h, const char* name, const float* data, const int64_t* shape,
+                     int ndim) {
+    if (!h || !name) return fail(WRNN_ERR_INVALID, "null argument");
+    auto it = h->expected.find(name);
+    if (it == h->expected.end()) return WRNN_OK;  // e.g. "step", num_batches_tracked
+    if (!data || !shape) return fail(WRNN_ERR_INVALID, "null data");
+    const auto& ex = it->second;
+    bool ok = (int)ex.size() == ndim;
+    for (int i = 0; ok && i < ndim; ++i) ok = ex[i] == shape[i];
+    if (!ok) {
+        std::string s = "size mismatch for " + std::string(name) + ": expected (";
+        for (size_t i = 0; i < ex.size(); ++i) s += std::to_string(ex[i]) + (i + 1 < ex.size() ? ", " : "");
+        s += ") got (";
+        for (int i = 0; i < ndim; ++i) s += std::to_string(shape[i]) + (i + 1 < ndim ? ", " : "");
+        return fail(WRNN_ERR_INVALID, s + ")");
+    }
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
+    h->host[name].assign(data, data + n);
+    h->finalized = false;
+    return WRNN_OK;
+}
+
+int wrnn_finalize(wrnn_handle* h) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    HIPC(hipSetDevice(h->device));
+    return do_finalize(h);
+}
+
+int wrnn_set_seed(wrnn_handle* h, uint64_t seed) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    h->seed = seed;
+    h->stream_ctr = 0;
+    return WRNN_OK;
+}
+
+int wrnn_set_stream(wrnn_handle* h, uint32_t stream) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    h->stream_ctr = stream;
+    return WRNN_OK;
+}
+
+int wrnn_fold_shape(int n_frames, int hop_length, int batched, int target, int overlap,
+                    int* num_folds, int* seq_len) {
+    if (!num_folds || !seq_len) return fail(WRNN_ERR_INVALID, "null argument");
+    if (n_frames <= 0 || hop_length <= 0) return fail(WRNN_ERR_INVALID, "bad length");
+    if (batched && (target <= 0 || overlap < 0)) return fail(WRNN_ERR_INVALID, "bad target/overlap");
+    fold_shape(n_frames * hop_length, batched, target, overlap, num_folds, seq_len);
+    return WRNN_OK;
+}
+
+int wrnn_generate(wrnn_handle* h, const float* mel, int n_frames, int batched, int target,
+                  int overlap, int16_t* labels, float* samples, size_t capacity, int* num_folds,
+                  int* seq_len, wrnn_progress_fn cb, void* user) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (!h->finalized)
+        return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
+    if (!mel || n_frames <= 0) return fail(WRNN_ERR_INVALID, "empty mel");
+    if (labels && h->cfg.mode != WRNN_MODE_RAW) return fail(WRNN_ERR_INVALID, "labels require RAW mode");
+    HIPC(hipSetDevice(h->device));
+    int B, S;
+    fold_shape(n_frames * h->hop, batched, target, overlap, &B, &S);
+    if (B <= 0) return fail(WRNN_ERR_INVALID, "mel too short for target/overlap");
+    if ((labels || samples) && capacity < (size_t)B * S)
+        return fail(WRNN_ERR_CAPACITY, "output capacity " + std::to_string(capacity) + " < " +
+                                           std::to_string((size_t)B * S));
+    auto& ws = h->ws;
+    const size_t mbytes = (size_t)h->feat * n_frames * sizeof(float);
+    if (mbytes > ws.mel_in.bytes) {
+        ws.mel_in.release();
+        CHECK(ws.mel_in.alloc(mbytes));
+    }
+    HIPC(hipMemcpyAsync(ws.mel_in.p, mel, mbytes, hipMemcpyHostToDevice, h->stream));
+    const float* mels[1] = {ws.mel_in.f()};
+    int roff[2];
+    int S2 = 0;
+    CHECK(generate_impl(h, 1, mels, &n_frames, batched, target, overlap, roff, &S2, cb, user));
+    // copy rows out (device row stride = ws.S)
+    if (labels)
+        HIPC(hipMemcpy2DAsync(labels, S * sizeof(int16_t), ws.labels.p, ws.S * sizeof(int16_t),
+                              S * sizeof(int16_t), B, hipMemcpyDeviceToHost, h->stream));
+    if (samples)
+        HIPC(hipMemcpy2DAsync(samples, S * sizeof(float), ws.samples.p, ws.S * sizeof(float),
+                              S * sizeof(float), B, hipMemcpyDeviceToHost, h->stream));
+    HIPC(hipStreamSynchronize(h->stream));
+    CHECK(collect_timing(h));
+    if (num_folds) *num_folds = B;
+    if (seq_len) *seq_len = S;
+    return WRNN_OK;
+}
+
+int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* mels,
+                               const int* n_frames, int batched, int target, int overlap,
+                               int16_t* labels_dev, float* samples_dev, size_t capacity,
+                               int* row_offset, int* seq_len, wrnn_progress_fn cb, void* user) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (!mels || !n_frames || !row_offset) return fail(WRNN_ERR_INVALID, "null argument");
+    if (labels_dev && h->cfg.mode != WRNN_MODE_RAW)
+        return fail(WRNN_ERR_INVALID, "labels require RAW mode");
+    HIPC(hipSetDevice(h->device));
+    int B = 0, S = 0;
+    for (int u = 0; u < n_utts; ++u) {
+        int b, s;
+        if (n_frames[u] <= 0) return fail(WRNN_ERR_INVALID, "empty mel");
+        fold_shape(n_frames[u] * h->hop, batched, target, overlap, &b, &s);
+        B += b;
+        S = s;
+    }
+    if ((labels_dev || samples_dev) && capacity < (size_t)B * S)
+        return fail(WRNN_ERR_CAPACITY, "output capacity too small");
+    int S2 = 0;
+    CHECK(generate_impl(h, n_utts, mels, n_frames, batched, target, overlap, row_offset, &S2, cb, user));
+    auto& ws = h->ws;
+    if (labels_dev)
+        HIPC(hipMemcpy2DAsync(labels_dev, S * sizeof(int16_t), ws.labels.p, ws.S * sizeof(int16_t),
+                              S * sizeof(int16_t), B, hipMemcpyDeviceToDevice, h->stream));
+    if (samples_dev)
+        HIPC(hipMemcpy2DAsync(samples_dev, S * sizeof(float), ws.samples.p, ws.S * sizeof(float),
+                              S * sizeof(float), B, hipMemcpyDeviceToDevice, h->stream));
+    HIPC(hipStreamSynchronize(h->stream));
+    CHECK(collect_timing(h));
+    if (seq_len) *seq_len = S;
+    return WRNN_OK;
+}
+
+int wrnn_enable_stage_timing(wrnn_handle* h, int enable) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    h->timing = enable != 0;
+    return WRNN_OK;
+}
+
+int wrnn_stage_timing(wrnn_handle* h, int stage, double* avg_us, int* launches) {
+    if (!h || !avg_us || !launches) return fail(WRNN_ERR_INVALID, "null argument");
+    if (stage < 0 || stage >= (int)h->stage_avg_us.size())
+        return fail(WRNN_ERR_INVALID, "no timing for stage " + std::to_string(stage));
+    *avg_us = h->stage_avg_us[stage];
+    *launches = h->stage_launches[stage];
+    return WRNN_OK;
+}
+
+int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, double* bytes,
+                    double* flops, int* n_stages) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (n_stages) *n_stages = (int)h->stages.size();
+    if (stage < 0 || stage >= (int)h->stages.size())
+        return fail(WRNN_ERR_INVALID, "bad stage index");
+    const StageDesc& sd = h->stages[stage];
+    if (name && name_cap) {
+        std::snprintf(name, name_cap, "%s", sd.name.c_str());
+    }
+    const double B = h->last_B;
+    double by = 0, fl = 0;
+    for (const SegDesc& d : sd.segs) {
+        const double n = d.w.n_out, K = d.w.K;
+        by += n * K * 4.0;             // weights
+        by += B * K * 4.0;             // input rows
+        by += B * n * 4.0;             // outputs / gate pre-activations consumed
+        if (d.kind == EPI_GRU) by += B * (3 * h->H + 3 * h->H + 2 * h->H) * 4.0;  // cond,gh,h,xout
+        else by += B * n * 4.0;        // cond / bias read
+        fl += 2.0 * n * K * B;
+    }
+    if (bytes) *bytes = by;
+    if (flops) *flops = fl;
+    return WRNN_OK;
+}
+
+int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity) {
+    if (!h || !out) return fail(WRNN_ERR_INVALID, "null argument");
+    if (h->cfg.mode != WRNN_MODE_RAW) return fail(WRNN_ERR_INVALID, "RAW mode only");
+    const size_t n = (size_t)n_steps * h->last_B * h->n_classes;
+    if (n_steps > h->last_S || capacity < n) return fail(WRNN_ERR_CAPACITY, "capacity");
+    HIPC(hipStreamSynchronize(h->stream));
+    HIPC(hipMemcpy(out, h->ws.noise.p, n * sizeof(float), hipMemcpyDeviceToHost));
+    return WRNN_OK;
+}
+
+int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* aux_out,
+                        size_t aux_cap) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    HIPC(hipStreamSynchronize(h->stream));
+    const size_t nm = (size_t)h->feat * h->last_L0, na = (size_t)h->R * h->last_T0;
+    if (mel_out) {
+        if (mel_cap < nm) return fail(WRNN_ERR_CAPACITY, "mel capacity");
+        HIPC(hipMemcpy(mel_out, h->ws.melup.p, nm * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    if (aux_out) {
+        if (aux_cap < na) return fail(WRNN_ERR_CAPACITY, "aux capacity");
+        HIPC(hipMemcpy(aux_out, h->ws.Rb.p, na * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return WRNN_OK;
+}
+
+}  // extern "C"

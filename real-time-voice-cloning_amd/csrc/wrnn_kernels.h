@@ -1,0 +1,134 @@
+// Internal declarations shared by the HIP kernels (kernels_*.hip) and the runtime
+// (runtime.hip). Not part of the public ABI (include/wavernn_mi355x.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wrnn {
+
+constexpr int kThreads = 256;  // every kernel: 4 wave64 per workgroup
+
+// ---------------------------------------------------------------------------------------
+// Recurrent step ("stage") kernels. One launch = up to 3 matvec segments that are
+// independent of each other (a critical-path layer plus off-path recurrent products).
+// ---------------------------------------------------------------------------------------
+enum EpiKind : int {
+    EPI_GRU = 0,        // torch GRUCell gates -> h (in place) and x_out = x_in + h
+    EPI_BIAS3 = 1,      // out[r][g*H + j] = acc + bias  (W_hh h + b_hh ; W_ih1 cI + b_ih1)
+    EPI_COND = 2,       // out[r][o] = acc + cond(frame)[o]
+    EPI_COND_RELU = 3,  // out[r][o] = relu(acc + cond(frame)[o])
+};
+
+// Tile shapes: OPL outputs per thread, NOG output groups per tile, KC = 256/NOG k-chunks.
+enum TileCfg : int {
+    CFG3 = 0,  // OPL 3 (the r,z,n gates of one unit), 4 units per tile  (OT 12)
+    CFG2 = 1,  // OPL 2, 8 groups (OT 16)
+    CFG1 = 2,  // OPL 1, 4 groups (OT 4)
+};
+
+struct RowInfo {
+    int pos0;        // global index of this row's step-0 position in per-position buffers
+    int rel0;        // fold start inside its utterance: fold * (target + overlap)
+    int L;           // valid upsampled length of its utterance (positions >= L are pad)
+    int fbase;       // per-frame buffers: frame slot of the utterance's zero frame
+    int fold;        // fold index inside its utterance (Philox counter word 2)
+    uint32_t stream; // Philox counter word 3 of its utterance
+};
+
+struct Seg {
+    const float* W;  // packed tiles, see pack_segment() in runtime.hip
+    int n_out, n_tiles, kind, cfg;
+    // input row r: X + x_off + r * x_ld + rows[r].pos0 * x_pld
+    const float* X;
+    long long x_off;
+    int x_ld, x_pld;
+    // outputs
+    float* Y;
+    int y_ld;
+    const float* cond;  // row r: cond + frame(r) * c_ld   (c_ld == 0: one shared vector)
+    int c_ld;
+    const float* gh;    // EPI_GRU: W_hh h_prev + b_hh, [r][3H] gate-major
+    float* h;           // EPI_GRU: hidden state [r][H], updated in place
+    float* xout;        // EPI_GRU: x_in + h_new, [r][H]
+    int H;
+};
+
+struct StageArgs {
+    Seg seg[3];
+    int nseg;
+    int tile_start[4];  // blockIdx.x ranges per segment
+    int nrows;
+    int t;              // step index (selects frames of the conditioning)
+    int hop;
+    const RowInfo* rows;
+    uint32_t* stamps;   // optional: workgroup w stores [2w] = start, [2w+1] = end
+                        // (low 32 bits of s_memrealtime, 100 MHz) -- no atomics
+};
+
+constexpr int kMaxStampWG = 2048;  // workgroups recorded per timed launch
+constexpr int kStampEvery = 8;     // timed steps: t % kStampEvery == 0
+
+struct SampleArgs {
+    int t;          // step whose logits are sampled; -1 = initial GRU1 only (x = 0)
+    int S, nrows, n_classes, mode, H;
+    const float* logits;   // [r][n_classes]
+    const float* noise;    // RAW: [t][r][n_classes] Exp(1) variates
+    float* samples;        // [r][S]
+    int16_t* labels;       // [r][S] (RAW)
+    int do_gru;            // compute GRU1 of step t+1
+    const float* P1;       // [r][3H] = W_ih1 cI(t+1) + b_ih1
+    const float* v;        // [3H]    = W_ih1 . I.weight[:,0]
+    const float* gh1;      // [r][3H] = W_hh1 h1 + b_hh1
+    float* h1;             // [r][H] in/out
+    float* x1;             // [r][H] out: xI + h1
+    const float* cI;       // per position [p][H]: I.weight[:,1:] . [m, a1[:31]] + I.bias
+    const float* w0;       // [H] = I.weight[:, 0]
+    const RowInfo* rows;
+    uint32_t k0, k1;       // Philox key (MOL draws in-kernel)
+};
+
+// ---------------------------------------------------------------------------------------
+// GEMM-shaped precompute (upsample convs + conditioning), fp32 MFMA 32x32x2.
+// D[m][n] = sum_k A(m,k) * B(k,n), epilogue per element.
+// ---------------------------------------------------------------------------------------
+struct GemmA {  // A(m, k)
+    int kind;   // 0: row-major W[m*ld + k]; 1: cond-A (mel/aux gather for cI); 2: frame-A
+    const float* p;
+    int ld;
+    // kind 1: mel_up channel-major [80][ldm] + R channel-major [C][T]
+    const float* mel;
+    int ldm, n_mel, L, hop;
+    const float* R;
+    int ldr, r_off, n_aux;
+};
+struct GemmB {  // B(k, n)
+    int kind;   // 0: row-major [k*ld + n]; 1: im2col of the zero-padded mel (conv_in)
+    const float* p;
+    int ld;
+    int T, pad, ksz;  // kind 1
+};
+struct GemmEp {
+    int kind;   // 0: +bias[n]; 1: +bias[m]; 2: BN(m) [+relu] [+res]
+    float* D;
+    int ld;
+    const float* bias;
+    const float* alpha;
+    const float* beta;
+    const float* res;
+    int relu;
+};
+
+// launch wrappers (kernels_*.hip); return hipError_t
+hipError_t launch_stage(const StageArgs& a, int K, int RT, int n_row_tiles, hipStream_t s);
+hipError_t prepare_stage(int K, int RT);  // set the dynamic-LDS attribute (before capture)
+hipError_t launch_sample(const SampleArgs& a, hipStream_t s);
+hipError_t launch_noise_raw(float* q, int S, int nrows, int n_classes, const RowInfo* rows,
+                            uint32_t k0, uint32_t k1, hipStream_t s);
+hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, const GemmEp& e,
+                       hipStream_t s);
+hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, float* out,
+                              int scale, const float* w, int c, int out_lo, int out_len,
+                              int ld_out, hipStream_t s);
+hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipStream_t s);
+
+}  // namespace wrnn

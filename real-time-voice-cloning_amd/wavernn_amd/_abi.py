@@ -1,0 +1,120 @@
+"""ctypes bindings of libwavernn_mi355x.so (include/wavernn_mi355x.h).
+
+The library is the only compute path of this package: if it is missing, importing the model
+raises immediately -- there is no CPU or eager-PyTorch fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = 'libwavernn_mi355x.so'
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+WRNN_OK = 0
+WRNN_ERR_INVALID = -1
+WRNN_ERR_NOT_LOADED = -2
+WRNN_ERR_HIP = -3
+WRNN_ERR_OOM = -4
+WRNN_ERR_ABORTED = -5
+WRNN_ERR_CAPACITY = -6
+
+WRNN_MODEL_FATCHORD = 0
+WRNN_MODEL_RUNTIMERACER = 1
+WRNN_MODE_RAW = 0
+WRNN_MODE_MOL = 1
+
+EXPORTED = [
+    'wrnn_version', 'wrnn_last_error', 'wrnn_device_count', 'wrnn_create', 'wrnn_destroy',
+    'wrnn_load_tensor', 'wrnn_finalize', 'wrnn_set_seed', 'wrnn_set_stream', 'wrnn_fold_shape',
+    'wrnn_generate', 'wrnn_generate_batch_device', 'wrnn_enable_stage_timing',
+    'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
+]
+
+
+class WrnnConfig(ctypes.Structure):
+    _fields_ = [
+        ('model_type', ctypes.c_int), ('mode', ctypes.c_int), ('bits', ctypes.c_int),
+        ('rnn_dims', ctypes.c_int), ('fc_dims', ctypes.c_int), ('compute_dims', ctypes.c_int),
+        ('res_out_dims', ctypes.c_int), ('res_blocks', ctypes.c_int), ('pad', ctypes.c_int),
+        ('feat_dims', ctypes.c_int), ('hop_length', ctypes.c_int), ('n_upsample', ctypes.c_int),
+        ('upsample_factors', ctypes.c_int * 4),
+    ]
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int, ctypes.c_double)
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load_library(path=None):
+    """Load (once) and type the C-ABI library. Raises NativeLibraryMissing if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f'{LIB_NAME} not found at {path}: build it with `make -C '
+            f'real-time-voice-cloning_amd/csrc` or __graft_entry__.build(); the MI355X vocoder '
+            f'has no CPU fallback')
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    sig = {
+        'wrnn_version': (ctypes.c_char_p, []),
+        'wrnn_last_error': (ctypes.c_char_p, []),
+        'wrnn_device_count': (c_int, [P(c_int)]),
+        'wrnn_create': (c_int, [P(WrnnConfig), c_int, P(c_void_p)]),
+        'wrnn_destroy': (None, [c_void_p]),
+        'wrnn_load_tensor': (c_int, [c_void_p, ctypes.c_char_p, P(ctypes.c_float),
+                                     P(ctypes.c_int64), c_int]),
+        'wrnn_finalize': (c_int, [c_void_p]),
+        'wrnn_set_seed': (c_int, [c_void_p, ctypes.c_uint64]),
+        'wrnn_set_stream': (c_int, [c_void_p, ctypes.c_uint32]),
+        'wrnn_fold_shape': (c_int, [c_int, c_int, c_int, c_int, c_int, P(c_int), P(c_int)]),
+        'wrnn_generate': (c_int, [c_void_p, P(ctypes.c_float), c_int, c_int, c_int, c_int,
+                                  P(ctypes.c_int16), P(ctypes.c_float), c_size_t, P(c_int),
+                                  P(c_int), PROGRESS_FN, c_void_p]),
+        'wrnn_generate_batch_device': (c_int, [c_void_p, c_int, P(c_void_p), P(c_int), c_int,
+                                               c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                               P(c_int), P(c_int), PROGRESS_FN, c_void_p]),
+        'wrnn_enable_stage_timing': (c_int, [c_void_p, c_int]),
+        'wrnn_stage_timing': (c_int, [c_void_p, c_int, P(ctypes.c_double), P(c_int)]),
+        'wrnn_stage_info': (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t,
+                                    P(ctypes.c_double), P(ctypes.c_double), P(c_int)]),
+        'wrnn_debug_noise': (c_int, [c_void_p, c_int, P(ctypes.c_float), c_size_t]),
+        'wrnn_debug_upsample': (c_int, [c_void_p, P(ctypes.c_float), c_size_t,
+                                        P(ctypes.c_float), c_size_t]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def last_error():
+    return load_library().wrnn_last_error().decode('utf-8', 'replace')
+
+
+def check(rc, what=''):
+    """Raise the reference's exception type for a failed call (WaveRNNVocoder.cpp:24-41)."""
+    if rc == WRNN_OK:
+        return
+    msg = last_error()
+    if what:
+        msg = f'{what}: {msg}'
+    if rc == WRNN_ERR_INVALID:
+        raise ValueError(msg)
+    if rc == WRNN_ERR_OOM:
+        raise MemoryError(msg)
+    if rc == WRNN_ERR_ABORTED:
+        raise KeyboardInterrupt(msg)
+    raise RuntimeError(msg)

@@ -1,0 +1,90 @@
+"""Host-side f64 post-processing of the vocoder output (restated from the reference).
+
+* ``label_2_float``  vocoder/audio.py:9-10
+* ``decode_mu_law``  vocoder/audio.py:102-107
+* ``de_emphasis``    vocoder/audio.py:92-93 (scipy.signal.lfilter, same call)
+* ``xfade_and_unfold`` vocoder/models/fatchord_version.py:342-404
+* ``fade_out_tail``  vocoder/models/fatchord_version.py:252-255
+
+These run on the host in float64 exactly as the reference does (same numpy/scipy calls in the
+same order), so given identical per-fold samples the waveform is bit-identical.
+"""
+import math
+
+import numpy as np
+from scipy.signal import lfilter
+
+from .hparams import sp
+
+
+def label_2_float(x, bits):
+    return 2 * x / (2 ** bits - 1.) - 1.
+
+
+def labels_to_samples(labels, n_classes):
+    """torch ``2 * k.float() / (n_classes - 1.) - 1.`` in fp32 (fatchord_version.py:228)."""
+    k = labels.astype(np.float32)
+    return (np.float32(2) * k) / np.float32(n_classes - 1.) - np.float32(1.)
+
+
+def decode_mu_law(y, mu, from_labels=True):
+    if from_labels:
+        y = label_2_float(y, math.log2(mu))
+    mu = mu - 1
+    x = np.sign(y) / mu * ((1 + mu) ** np.abs(y) - 1)
+    return x
+
+
+def encode_mu_law(x, mu):
+    mu = mu - 1
+    fx = np.sign(x) * np.log(1 + mu * np.abs(x)) / np.log(1 + mu)
+    return np.floor((fx + 1) / 2 * mu + 0.5)
+
+
+def de_emphasis(x):
+    return lfilter([1], [1, -sp.preemphasis], x)
+
+
+def pre_emphasis(x):
+    return lfilter([1, -sp.preemphasis], [1], x)
+
+
+def xfade_and_unfold(y, target, overlap):
+    """Equal-power cross-fade of the fold rows, overlap-added into one signal (f64)."""
+    num_folds, length = y.shape
+    target = length - 2 * overlap
+    total_len = num_folds * (target + overlap) + overlap
+    silence_len = overlap // 2
+    fade_len = overlap - silence_len
+    silence = np.zeros((silence_len), dtype=np.float64)
+    t = np.linspace(-1, 1, fade_len, dtype=np.float64)
+    fade_in = np.sqrt(0.5 * (1 + t))
+    fade_out = np.sqrt(0.5 * (1 - t))
+    fade_in = np.concatenate([silence, fade_in])
+    fade_out = np.concatenate([fade_out, silence])
+    y[:, :overlap] *= fade_in
+    y[:, -overlap:] *= fade_out
+    unfolded = np.zeros((total_len), dtype=np.float64)
+    for i in range(num_folds):
+        start = i * (target + overlap)
+        end = start + target + 2 * overlap
+        unfolded[start:end] += y[i]
+    return unfolded
+
+
+def postprocess(samples, batched, target, overlap, mu_law, apply_preemphasis, n_classes,
+                wave_len, hop_length):
+    """fatchord_version.py:238-255 on the (B, S) per-fold samples (any float dtype)."""
+    output = np.asarray(samples).astype(np.float64)
+    if batched:
+        output = xfade_and_unfold(output, target, overlap)
+    else:
+        output = output[0]
+    if mu_law:
+        output = decode_mu_law(output, n_classes, False)
+    if apply_preemphasis:
+        output = de_emphasis(output)
+    fade_out = np.linspace(1, 0, 20 * hop_length)
+    output = output[:wave_len]
+    output[-20 * hop_length:] *= fade_out
+    return output

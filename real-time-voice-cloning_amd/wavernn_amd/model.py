@@ -1,0 +1,298 @@
+"""WaveRNN facade over the MI355X library: same constructor and ``generate`` as the reference.
+
+Mirrors ``vocoder/models/fatchord_version.py:88-259`` / ``runtimeracer_version.py:98-314``:
+``WaveRNN(rnn_dims, fc_dims, bits, pad, upsample_factors, feat_dims, compute_dims, res_out_dims,
+res_blocks, hop_length, sample_rate, mode)`` plus ``model_type`` (which of the two topologies),
+``load_state_dict`` with the reference's state-dict names, and
+``generate(mels, batched, target, overlap, mu_law, apply_preemphasis, progress_callback)``
+returning the float64 waveform of ``(T - 1) * hop_length`` samples.
+
+The whole recurrence (upsample network, conditioning, GRU/FC steps, sampling) runs on the GPU
+through the C-ABI; only the reference's f64 post-processing (cross-fade, mu-law, de-emphasis,
+fade-out; fatchord_version.py:238-255) runs on the host, restated bit-exactly in audio.py.
+"""
+import ctypes
+import sys
+import time
+
+import numpy as np
+
+from . import _abi
+from .audio import labels_to_samples, postprocess
+
+MODEL_TYPE_FATCHORD = 'fatchord-wavernn'
+MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
+_MODEL_IDS = {MODEL_TYPE_FATCHORD: _abi.WRNN_MODEL_FATCHORD,
+              MODEL_TYPE_RUNTIMERACER: _abi.WRNN_MODEL_RUNTIMERACER}
+
+
+def _progbar(i, n, size=16):
+    done = (i * size) // n
+    return ''.join('█' if j <= done else '░' for j in range(size))
+
+
+def _to_numpy_f32(x):
+    if hasattr(x, 'detach'):
+        x = x.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+
+
+class WaveRNN:
+    def __init__(self, rnn_dims, fc_dims, bits, pad, upsample_factors, feat_dims, compute_dims,
+                 res_out_dims, res_blocks, hop_length, sample_rate, mode='RAW', pruning=False,
+                 model_type=MODEL_TYPE_FATCHORD, device=0):
+        if mode == 'RAW':
+            self.n_classes = 2 ** bits
+        elif mode == 'MOL':
+            self.n_classes = 30
+        else:
+            raise RuntimeError("Unknown model mode value - ", mode)
+        if model_type not in _MODEL_IDS:
+            raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
+        self.mode = mode
+        self.bits = bits
+        self.pad = pad
+        self.rnn_dims = rnn_dims
+        self.fc_dims = fc_dims
+        self.aux_dims = res_out_dims // 4
+        self.hop_length = hop_length
+        self.sample_rate = sample_rate
+        self.model_type = model_type
+        self.upsample_factors = tuple(upsample_factors)
+        self.device = device
+        self._step = 0
+        self._lib = _abi.load_library()
+        cfg = _abi.WrnnConfig()
+        cfg.model_type = _MODEL_IDS[model_type]
+        cfg.mode = _abi.WRNN_MODE_RAW if mode == 'RAW' else _abi.WRNN_MODE_MOL
+        cfg.bits = bits
+        cfg.rnn_dims, cfg.fc_dims = rnn_dims, fc_dims
+        cfg.compute_dims, cfg.res_out_dims = compute_dims, res_out_dims
+        cfg.res_blocks, cfg.pad = res_blocks, pad
+        cfg.feat_dims, cfg.hop_length = feat_dims, hop_length
+        cfg.n_upsample = len(self.upsample_factors)
+        for i, s in enumerate(self.upsample_factors):
+            cfg.upsample_factors[i] = s
+        self._cfg = cfg
+        h = ctypes.c_void_p()
+        _abi.check(self._lib.wrnn_create(ctypes.byref(cfg), int(device), ctypes.byref(h)),
+                   'wrnn_create')
+        self._h = h
+        self._loaded = False
+        self.timings = {}
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h is not None and h.value:
+            try:
+                self._lib.wrnn_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # --- torch.nn.Module-like surface used by the reference's callers -----------------
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        return self
+
+    def to(self, device):
+        return self
+
+    def get_step(self):
+        return self._step
+
+    def num_params(self, print_out=False):
+        return None
+
+    def load_state_dict(self, state_dict, strict=True):
+        """Upload a reference state dict (torch tensors or numpy arrays, PyTorch layout)."""
+        for name, value in state_dict.items():
+            if name == 'step':
+                self._step = int(np.asarray(value.cpu() if hasattr(value, 'cpu') else value)
+                                 .reshape(-1)[0])
+                continue
+            if name.endswith('num_batches_tracked'):
+                continue
+            arr = _to_numpy_f32(value)
+            shape = (ctypes.c_int64 * arr.ndim)(*arr.shape)
+            _abi.check(self._lib.wrnn_load_tensor(
+                self._h, name.encode(), arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                shape, arr.ndim), 'load_state_dict')
+        _abi.check(self._lib.wrnn_finalize(self._h), 'load_state_dict')
+        self._loaded = True
+
+    def set_seed(self, seed):
+        _abi.check(self._lib.wrnn_set_seed(self._h, ctypes.c_uint64(int(seed) & (2 ** 64 - 1))))
+
+    def set_stream(self, stream):
+        _abi.check(self._lib.wrnn_set_stream(self._h, ctypes.c_uint32(int(stream))))
+
+    def fold_shape(self, n_frames, batched, target, overlap):
+        b, s = ctypes.c_int(), ctypes.c_int()
+        _abi.check(self._lib.wrnn_fold_shape(int(n_frames), self.hop_length, int(bool(batched)),
+                                             int(target or 0), int(overlap or 0),
+                                             ctypes.byref(b), ctypes.byref(s)))
+        return b.value, s.value
+
+    def enable_stage_timing(self, enable=True):
+        _abi.check(self._lib.wrnn_enable_stage_timing(self._h, int(bool(enable))))
+
+    def stage_info(self):
+        """[(name, algorithmic bytes/launch, flops/launch, avg us, launches)] of the last call."""
+        n = ctypes.c_int()
+        name = ctypes.create_string_buffer(64)
+        by, fl = ctypes.c_double(), ctypes.c_double()
+        _abi.check(self._lib.wrnn_stage_info(self._h, 0, name, 64, ctypes.byref(by),
+                                             ctypes.byref(fl), ctypes.byref(n)))
+        out = []
+        for s in range(n.value):
+            _abi.check(self._lib.wrnn_stage_info(self._h, s, name, 64, ctypes.byref(by),
+                                                 ctypes.byref(fl), None))
+            us, cnt = ctypes.c_double(), ctypes.c_int()
+            rc = self._lib.wrnn_stage_timing(self._h, s, ctypes.byref(us), ctypes.byref(cnt))
+            out.append((name.value.decode(), by.value, fl.value,
+                        us.value if rc == 0 else float('nan'), cnt.value if rc == 0 else 0))
+        return out
+
+    def debug_noise(self, n_steps, n_rows):
+        """RAW Exp(1) noise of the last call, (n_steps, n_rows, n_classes) float32."""
+        out = np.empty((n_steps, n_rows, self.n_classes), dtype=np.float32)
+        _abi.check(self._lib.wrnn_debug_noise(self._h, n_steps,
+                                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                              out.size))
+        return out
+
+    def debug_upsample(self, n_frames, feat_dims=80, res_out_dims=None):
+        """(mel_up (feat, L), aux (res_out_dims, T)) of the last call's first utterance."""
+        R = res_out_dims or self.aux_dims * 4
+        L = n_frames * self.hop_length
+        mel = np.empty((feat_dims, L), dtype=np.float32)
+        aux = np.empty((R, n_frames), dtype=np.float32)
+        fp = ctypes.POINTER(ctypes.c_float)
+        _abi.check(self._lib.wrnn_debug_upsample(self._h, mel.ctypes.data_as(fp), mel.size,
+                                                 aux.ctypes.data_as(fp), aux.size))
+        return mel, aux
+
+    def gen_display(self, i, seq_len, b_size, gen_rate):
+        pbar = _progbar(i, seq_len)
+        msg = f'| {pbar} {i*b_size}/{seq_len*b_size} | Batch Size: {b_size} | Gen Rate: {gen_rate:.1f}kHz | '
+        sys.stdout.write(f"\r{msg}")
+
+    # --- the hot path ------------------------------------------------------------------
+    def generate_rows(self, mels, batched, target, overlap, progress_callback=None):
+        """Device recurrence only: returns (labels or None, samples (B,S) f32, B, S)."""
+        if not self._loaded:
+            raise RuntimeError("Model hasn't been loaded. Call loadWeights first.")
+        mel = _to_numpy_f32(mels)
+        if mel.ndim == 3:
+            mel = mel[0]
+        mel = np.ascontiguousarray(mel)
+        T = mel.shape[-1]
+        B, S = self.fold_shape(T, batched, target, overlap)
+        n = B * S
+        labels = np.empty((B, S), dtype=np.int16) if self.mode == 'RAW' else None
+        samples = None if self.mode == 'RAW' else np.empty((B, S), dtype=np.float32)
+        cb_ref = [None]
+
+        if progress_callback is not None:
+            def _cb(user, i, seq_len, b_size, rate):
+                try:
+                    progress_callback(i, seq_len, b_size, rate)
+                except Exception as e:  # surface callback errors after the call
+                    cb_ref[0] = e
+                    return 1
+                return 0
+            cfn = _abi.PROGRESS_FN(_cb)
+        else:
+            cfn = _abi.PROGRESS_FN()
+        ob, os_ = ctypes.c_int(), ctypes.c_int()
+        rc = self._lib.wrnn_generate(
+            self._h, mel.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), T,
+            int(bool(batched)), int(target or 0), int(overlap or 0),
+            labels.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)) if labels is not None else None,
+            samples.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if samples is not None else None,
+            n, ctypes.byref(ob), ctypes.byref(os_), cfn, None)
+        if cb_ref[0] is not None:
+            raise cb_ref[0]
+        _abi.check(rc, 'generate')
+        if labels is not None:
+            samples = labels_to_samples(labels, self.n_classes)
+        return labels, samples, B, S
+
+    def generate_batch_device(self, mels_dev, batched, target, overlap, progress_callback=None):
+        """Several utterances as one batch of fold rows, inputs resident in HBM.
+
+        ``mels_dev``: list of torch CUDA float32 tensors (feat_dims, T_u) on this model's device
+        (already normalised). Returns (out_dev, row_offset, S): ``out_dev`` is a torch CUDA
+        tensor (rows, S) -- int16 labels (RAW) or float32 samples (MOL).
+        """
+        import torch
+        if not self._loaded:
+            raise RuntimeError("Model hasn't been loaded. Call loadWeights first.")
+        n = len(mels_dev)
+        mels_dev = [m.contiguous() for m in mels_dev]
+        for m in mels_dev:
+            if m.dtype != torch.float32 or not m.is_cuda:
+                raise ValueError('mels must be float32 CUDA tensors')
+        frames = (ctypes.c_int * n)(*[int(m.shape[-1]) for m in mels_dev])
+        ptrs = (ctypes.c_void_p * n)(*[m.data_ptr() for m in mels_dev])
+        rows = 0
+        S = 0
+        for m in mels_dev:
+            b, S = self.fold_shape(int(m.shape[-1]), batched, target, overlap)
+            rows += b
+        dev = mels_dev[0].device
+        if self.mode == 'RAW':
+            out = torch.empty((rows, S), dtype=torch.int16, device=dev)
+            lab_p, smp_p = out.data_ptr(), None
+        else:
+            out = torch.empty((rows, S), dtype=torch.float32, device=dev)
+            lab_p, smp_p = None, out.data_ptr()
+        roff = (ctypes.c_int * (n + 1))()
+        s_out = ctypes.c_int()
+        cfn = _abi.PROGRESS_FN()
+        if progress_callback is not None:
+            cfn = _abi.PROGRESS_FN(lambda u, i, sl, b, r: (progress_callback(i, sl, b, r), 0)[1])
+        torch.cuda.current_stream(dev).synchronize()
+        rc = self._lib.wrnn_generate_batch_device(
+            self._h, n, ptrs, frames, int(bool(batched)), int(target or 0), int(overlap or 0),
+            lab_p, smp_p, rows * S, roff, ctypes.byref(s_out), cfn, None)
+        _abi.check(rc, 'generate_batch_device')
+        return out, list(roff), S
+
+    def generate_batch(self, mels_dev, batched, target, overlap, mu_law, apply_preemphasis,
+                       progress_callback=None):
+        """generate() for several device-resident mels; returns a list of f64 waveforms."""
+        mu_law = mu_law if self.mode == 'RAW' else False
+        out, roff, S = self.generate_batch_device(mels_dev, batched, target, overlap,
+                                                  progress_callback)
+        host = out.cpu().numpy()
+        wavs = []
+        for u, m in enumerate(mels_dev):
+            rows = host[roff[u]:roff[u + 1]]
+            smp = labels_to_samples(rows, self.n_classes) if self.mode == 'RAW' else rows
+            wave_len = (int(m.shape[-1]) - 1) * self.hop_length
+            wavs.append(postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
+                                    self.n_classes, wave_len, self.hop_length))
+        return wavs
+
+    def generate(self, mels, batched, target, overlap, mu_law, apply_preemphasis,
+                 progress_callback=None):
+        """fatchord_version.py:155-259 (runtimeracer_version.py:199-314) on the MI355X."""
+        mu_law = mu_law if self.mode == 'RAW' else False
+        progress_callback = progress_callback or self.gen_display
+        mel = _to_numpy_f32(mels)
+        T = mel.shape[-1]
+        wave_len = (T - 1) * self.hop_length
+        t0 = time.time()
+        labels, samples, B, S = self.generate_rows(mel, batched, target, overlap,
+                                                   progress_callback)
+        t1 = time.time()
+        out = postprocess(samples, batched, target, overlap, mu_law, apply_preemphasis,
+                          self.n_classes, wave_len, self.hop_length)
+        self.timings = dict(device=t1 - t0, post=time.time() - t1, B=B, S=S)
+        self.last_labels = labels
+        self.last_samples = samples
+        return out

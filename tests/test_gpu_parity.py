@@ -1,0 +1,102 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden outputs and the
+oracle restatement. Bar (BASELINE.json north_star): RAW 9/10-bit labels bit-exact, waveform
+bit-exact (f64 post-processing is the reference's own numpy/scipy code); MOL float path within
+1e-4 RMS.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_case, golden_meta, hparams_of
+
+pytestmark = pytest.mark.gpu
+
+MOL_RMS_TOL = 1e-4
+
+
+def make_model(meta):
+    from wavernn_amd.model import WaveRNN
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_state_dict
+    hp = hparams_of(meta)
+    sd = synth_state_dict(hp, meta['model_type'], seed=meta['weight_seed'],
+                          logit_scale=meta['logit_scale'])
+    m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
+                hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
+                mode=hp.mode, model_type=meta['model_type'], device=0)
+    m.load_state_dict(sd)
+    m.set_seed(meta['noise_seed'])
+    return m, hp, sd
+
+
+def run_case(name):
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold = golden_case(name)
+    m, hp, sd = make_model(meta)
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    wav = m.generate(mel[None], meta['batched'], meta['target'], meta['overlap'], hp.mu_law,
+                     sp.preemphasize, progress_callback=lambda *a: None)
+    return meta, gold, m, wav
+
+
+def first_divergence(a, b):
+    d = np.argwhere(a != b)
+    return None if len(d) == 0 else tuple(d[np.argmin(d[:, 1])])
+
+
+RAW_CASES = [k for k, v in golden_meta().items() if v['mode'] == 'RAW']
+MOL_CASES = [k for k, v in golden_meta().items() if v['mode'] == 'MOL']
+
+
+@pytest.mark.parametrize('name', RAW_CASES)
+def test_raw_labels_and_wave_bit_exact(name):
+    meta, gold, m, wav = run_case(name)
+    lab = m.last_labels
+    assert lab.shape == gold['labels'].shape == (meta['num_folds'], meta['seq_len'])
+    agree = float((lab == gold['labels']).mean())
+    assert agree == 1.0, f'{name}: label agreement {agree}, first divergence (row, step) ' \
+                         f'{first_divergence(lab, gold["labels"])}'
+    assert wav.dtype == np.float64 and wav.shape == gold['wav'].shape
+    assert np.array_equal(wav, gold['wav'])
+
+
+@pytest.mark.parametrize('name', MOL_CASES)
+def test_mol_float_path_within_tolerance(name):
+    meta, gold, m, wav = run_case(name)
+    s = m.last_samples
+    rms = float(np.sqrt(np.mean((s.astype(np.float64) - gold['samples']) ** 2)))
+    rms_w = float(np.sqrt(np.mean((wav - gold['wav']) ** 2)))
+    assert rms <= MOL_RMS_TOL, f'{name}: per-fold sample RMS {rms}'
+    assert rms_w <= MOL_RMS_TOL, f'{name}: waveform RMS {rms_w}'
+
+
+def test_noise_matches_philox_contract():
+    from oracle import philox
+    meta, gold, m, wav = run_case('fatchord_raw9_tiny')
+    B = meta['num_folds']
+    n_steps = 64
+    q = m.debug_noise(n_steps, B)
+    ref = philox.raw_exp_noise(meta['noise_seed'], 0, np.arange(n_steps), np.arange(B), m.n_classes)
+    assert np.array_equal(q, ref)
+
+
+def test_upsample_network_matches_oracle():
+    import torch
+    from oracle.wavernn_oracle import OracleWaveRNN
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold, m, wav = run_case('fatchord_raw9_tiny')
+    T = meta['n_frames']
+    mel_up, aux = m.debug_upsample(T)
+    hp = hparams_of(meta)
+    from wavernn_amd.synth import synth_state_dict
+    sd = synth_state_dict(hp, meta['model_type'], seed=meta['weight_seed'])
+    o = OracleWaveRNN(sd, hp, meta['model_type'])
+    mel = torch.from_numpy(synth_mel(T, meta['mel_seed'])[None] / sp.max_abs_value)
+    with torch.no_grad():
+        padded = o.pad_tensor(mel.transpose(1, 2), pad=hp.pad, side='both').transpose(1, 2)
+        ref_aux = o.resnet(padded)[0].numpy()
+        ref_mel, _ = o.upsample(padded)
+    ref_mel = ref_mel[0].numpy().T
+    np.testing.assert_allclose(aux, ref_aux, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)

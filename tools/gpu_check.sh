@@ -1,0 +1,22 @@
+#!/bin/bash
+# One gpurun call: parity tests, smoke, bench, each under its own time limit. Stops on any
+# crash / timeout (exit codes other than 0 and pytest's 1 = "tests failed").
+set -u
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+run() {  # run <name> <timeout> cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -30 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-parity,smoke,bench}
+[[ ,$STEPS, == *,parity,* ]] && run parity 600 python -m pytest tests/test_gpu_parity.py -q -x -rA
+[[ ,$STEPS, == *,gputests,* ]] && run gputests 900 python -m pytest tests -m gpu -q -rA
+[[ ,$STEPS, == *,smoke,* ]] && run smoke 300 python __graft_entry__.py smoke
+[[ ,$STEPS, == *,bench,* ]] && run bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10
+exit 0
