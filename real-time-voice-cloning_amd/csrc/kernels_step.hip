@@ -68,44 +68,86 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
     constexpr int OPL = Tile<CFG>::OPL, NOG = Tile<CFG>::NOG;
     constexpr int KC = kThreads / NOG;
     constexpr int KR = K / KC;
+    constexpr int KCP = KC + 4;  // padded reduction row: conflict-free ds_read_b128 per row
+    constexpr int NX = (RT * (K / 4) + kThreads - 1) / kThreads;  // X float4 per thread
     static_assert(KR % 4 == 0, "k-chunk must be a multiple of 4");
+    static_assert(NOG * RT <= kThreads, "one epilogue pair per thread");
     const int tid = threadIdx.x;
     const int og = tid % NOG, kc = tid / NOG;
     const int nrows = a.nrows;
+    const int H = sg.H;
+    const bool gather = sg.x_pld != 0;
 
-    // 1. weight tile -> registers; packed [tile][kc][og][j][kk] == [tile][tid][j][kk]
-    float w[OPL][KR];
+    // ---- 1. issue every global load of this tile up front (latency overlaps) ------------
+    // weight tile -> registers; packed [tile][kc][og][j][kk] == [tile][tid][j][kk]
+    float4 wv[OPL * KR / 4];
     {
         const float4* wp = reinterpret_cast<const float4*>(
             sg.W + ((size_t)tile * kThreads + tid) * (size_t)(OPL * KR));
 #pragma unroll
-        for (int j = 0; j < OPL; ++j)
-#pragma unroll
-            for (int q = 0; q < KR / 4; ++q) {
-                const float4 v = wp[j * (KR / 4) + q];
-                w[j][4 * q + 0] = v.x;
-                w[j][4 * q + 1] = v.y;
-                w[j][4 * q + 2] = v.z;
-                w[j][4 * q + 3] = v.w;
-            }
+        for (int i = 0; i < OPL * KR / 4; ++i) wv[i] = wp[i];
     }
-
-    // 2. RT input rows -> LDS Xs[b][K] (rows past nrows are zero)
-    float4* Xs4 = reinterpret_cast<float4*>(lds);
-    for (int e = tid; e < RT * (K / 4); e += kThreads) {
+    // input rows -> registers (staged to LDS below)
+    float4 xv[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        const int e = tid + i * kThreads;
         const int b = e / (K / 4), q = e % (K / 4);
         const int r = row0 + b;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < nrows) {
-            const float* xr = sg.X + sg.x_off + (long long)r * sg.x_ld +
-                              (long long)a.rows[r].pos0 * sg.x_pld;
-            v = reinterpret_cast<const float4*>(xr)[q];
+        xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < RT * (K / 4) && r < nrows) {
+            long long off = sg.x_off + (long long)r * sg.x_ld;
+            if (gather) off += (long long)a.rows[r].pos0 * sg.x_pld;
+            xv[i] = reinterpret_cast<const float4*>(sg.X + off)[q];
         }
-        Xs4[e] = v;
+    }
+    // epilogue operands of this thread's (group, row) pair
+    const int pog = tid / RT, pb = tid % RT;
+    const int pr = row0 + pb;
+    const bool has_pair = tid < NOG * RT && pr < nrows;
+    float e_c[OPL], e_gh[3] = {0.f, 0.f, 0.f}, e_h = 0.f, e_x = 0.f;
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) e_c[j] = 0.f;
+    int e_u = 0;
+    if (has_pair) {
+        if constexpr (CFG == CFG3) {
+            e_u = tile * NOG + pog;
+            if (e_u < H) {
+                const float* cr = sg.cond;
+                if (sg.c_ld) cr += (size_t)frame_of(a.rows[pr], a.t, a.hop) * (size_t)sg.c_ld;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) e_c[j] = cr[j * H + e_u];
+                if (sg.kind == EPI_GRU) {
+                    const float* gh = sg.gh + (size_t)pr * 3 * H;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) e_gh[j] = gh[j * H + e_u];
+                    e_h = sg.h[(size_t)pr * H + e_u];
+                    long long off = sg.x_off + (long long)pr * sg.x_ld;
+                    if (gather) off += (long long)a.rows[pr].pos0 * sg.x_pld;
+                    e_x = sg.X[off + e_u];
+                }
+            }
+        } else {
+            const float* cr = sg.cond;
+            if (sg.c_ld) cr += (size_t)frame_of(a.rows[pr], a.t, a.hop) * (size_t)sg.c_ld;
+#pragma unroll
+            for (int j = 0; j < OPL; ++j) {
+                const int o = (tile * NOG + pog) * OPL + j;
+                e_c[j] = o < sg.n_out ? cr[o] : 0.f;
+            }
+        }
+    }
+
+    // ---- 2. stage X in LDS: Xs[b][K] ---------------------------------------------------
+    float4* Xs4 = reinterpret_cast<float4*>(lds);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        const int e = tid + i * kThreads;
+        if (e < RT * (K / 4)) Xs4[e] = xv[i];
     }
     __syncthreads();
 
-    // 3. partial dot products over this thread's k-chunk
+    // ---- 3. partial dot products over this thread's k-chunk (fma chain, ascending k) ----
     float acc[OPL][RT];
 #pragma unroll
     for (int j = 0; j < OPL; ++j)
@@ -115,74 +157,69 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
     for (int b = 0; b < RT; ++b) {
 #pragma unroll
         for (int q = 0; q < KR / 4; ++q) {
-            const float4 xv = Xs4[b * (K / 4) + kc * (KR / 4) + q];
+            const float4 x4 = Xs4[b * (K / 4) + kc * (KR / 4) + q];
 #pragma unroll
             for (int j = 0; j < OPL; ++j) {
+                const float4 w4 = wv[j * (KR / 4) + q];
                 float s = acc[j][b];
-                s = fmaf(w[j][4 * q + 0], xv.x, s);
-                s = fmaf(w[j][4 * q + 1], xv.y, s);
-                s = fmaf(w[j][4 * q + 2], xv.z, s);
-                s = fmaf(w[j][4 * q + 3], xv.w, s);
+                s = fmaf(w4.x, x4.x, s);
+                s = fmaf(w4.y, x4.y, s);
+                s = fmaf(w4.z, x4.z, s);
+                s = fmaf(w4.w, x4.w, s);
                 acc[j][b] = s;
             }
         }
     }
     __syncthreads();
 
-    // 4. partials -> LDS red[kc][og][j][b]
+    // ---- 4. partials -> LDS red[og][j][b][kc] (kc contiguous, rows padded) --------------
     float* red = lds;
 #pragma unroll
     for (int j = 0; j < OPL; ++j)
 #pragma unroll
-        for (int b = 0; b < RT; ++b) red[((kc * NOG + og) * OPL + j) * RT + b] = acc[j][b];
+        for (int b = 0; b < RT; ++b) red[((og * OPL + j) * RT + b) * KCP + kc] = acc[j][b];
     __syncthreads();
 
-    // 5. reduce over k-chunks (fixed order) and apply the epilogue
-    const int H = sg.H;
-    for (int p = tid; p < NOG * RT; p += kThreads) {
-        const int pog = p / RT, b = p % RT;
-        const int r = row0 + b;
-        if (r >= nrows) continue;
-        float s[OPL];
+    // ---- 5. reduce over k-chunks in kc order and apply the epilogue ---------------------
+    if (!has_pair) return;
+    float s[OPL];
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+        const float4* rp = reinterpret_cast<const float4*>(red + ((pog * OPL + j) * RT + pb) * KCP);
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < KC / 4; ++c) {
+            const float4 t4 = rp[c];
+            v += t4.x;
+            v += t4.y;
+            v += t4.z;
+            v += t4.w;
+        }
+        s[j] = v;
+    }
+    if constexpr (CFG == CFG3) {
+        if (e_u >= H) return;
+        if (sg.kind == EPI_GRU) {
+            const float gi_r = add_nc(s[0], e_c[0]);
+            const float gi_z = add_nc(s[1], e_c[1]);
+            const float gi_n = add_nc(s[2], e_c[2]);
+            const float hn = gru_cell(gi_r, gi_z, gi_n, e_gh[0], e_gh[1], e_gh[2], e_h);
+            sg.h[(size_t)pr * H + e_u] = hn;
+            sg.xout[(size_t)pr * H + e_u] = add_nc(e_x, hn);
+        } else {  // EPI_BIAS3
+            float* y = sg.Y + (size_t)pr * sg.y_ld;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) y[j * H + e_u] = add_nc(s[j], e_c[j]);
+        }
+    } else {
+        float* y = sg.Y + (size_t)pr * sg.y_ld;
 #pragma unroll
         for (int j = 0; j < OPL; ++j) {
-            float v = red[(pog * OPL + j) * RT + b];
-            for (int c = 1; c < KC; ++c) v += red[((c * NOG + pog) * OPL + j) * RT + b];
-            s[j] = v;
-        }
-        if constexpr (CFG == CFG3) {
-            const int u = tile * NOG + pog;  // unit
-            if (u * 3 >= sg.n_out) continue;
-            if (sg.kind == EPI_GRU) {
-                const float* cr =
-                    sg.cond + (size_t)frame_of(a.rows[r], a.t, a.hop) * (size_t)sg.c_ld;
-                const float gi_r = add_nc(s[0], cr[u]);
-                const float gi_z = add_nc(s[1], cr[H + u]);
-                const float gi_n = add_nc(s[2], cr[2 * H + u]);
-                const float* gh = sg.gh + (size_t)r * 3 * H;
-                const float hp = sg.h[(size_t)r * H + u];
-                const float hn = gru_cell(gi_r, gi_z, gi_n, gh[u], gh[H + u], gh[2 * H + u], hp);
-                const float* xr = sg.X + sg.x_off + (long long)r * sg.x_ld +
-                                  (long long)a.rows[r].pos0 * sg.x_pld;
-                sg.h[(size_t)r * H + u] = hn;
-                sg.xout[(size_t)r * H + u] = add_nc(xr[u], hn);
-            } else {  // EPI_BIAS3
-                float* y = sg.Y + (size_t)r * sg.y_ld;
-                y[u] = add_nc(s[0], sg.cond[u]);
-                y[H + u] = add_nc(s[1], sg.cond[H + u]);
-                y[2 * H + u] = add_nc(s[2], sg.cond[2 * H + u]);
-            }
-        } else {
-            const float* cr = sg.cond + (size_t)frame_of(a.rows[r], a.t, a.hop) * (size_t)sg.c_ld;
-            float* y = sg.Y + (size_t)r * sg.y_ld;
-#pragma unroll
-            for (int j = 0; j < OPL; ++j) {
-                const int o = (tile * NOG + pog) * OPL + j;
-                if (o < sg.n_out) {
-                    float v = add_nc(s[j], cr[o]);
-                    if (sg.kind == EPI_COND_RELU) v = v > 0.f ? v : 0.f;
-                    y[o] = v;
-                }
+            const int o = (tile * NOG + pog) * OPL + j;
+            if (o < sg.n_out) {
+                float v = add_nc(s[j], e_c[j]);
+                if (sg.kind == EPI_COND_RELU) v = v > 0.f ? v : 0.f;
+                y[o] = v;
             }
         }
     }
@@ -217,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
 template <int K, int RT>
 static size_t stage_lds_bytes() {
     const size_t xs = (size_t)RT * K * sizeof(float);
-    const size_t red = (size_t)kThreads * 3 * RT * sizeof(float);  // max OPL = 3
+    const size_t red = (size_t)4 * 3 * RT * (64 + 4) * sizeof(float);  // NOG*OPL*RT*KCP max
     return xs > red ? xs : red;
 }
 

@@ -415,7 +415,8 @@ int do_finalize(wrnn_handle* h) {
     if (H != F) return fail(WRNN_ERR_INVALID, "rnn_dims != fc_dims is not supported");
     if (K != 256 && K != 512)
         return fail(WRNN_ERR_INVALID, "rnn_dims must be 256 or 512 (got " + std::to_string(K) + ")");
-    if (n % 4) return fail(WRNN_ERR_INVALID, "n_classes must be a multiple of 4");
+    if (h->cfg.mode == WRNN_MODE_RAW && n % 4)
+        return fail(WRNN_ERR_INVALID, "n_classes must be a multiple of 4");
     auto seg_gru = [&](const std::string& gname, int col0_ld, int x, int gh, int hh, int xout,
                        const float* cond, int fc) {
         SegDesc s{};

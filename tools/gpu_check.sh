@@ -18,5 +18,6 @@ STEPS=${STEPS:-parity,smoke,bench}
 [[ ,$STEPS, == *,parity,* ]] && run parity 600 python -m pytest tests/test_gpu_parity.py -q -x -rA
 [[ ,$STEPS, == *,gputests,* ]] && run gputests 900 python -m pytest tests -m gpu -q -rA
 [[ ,$STEPS, == *,smoke,* ]] && run smoke 300 python __graft_entry__.py smoke
-[[ ,$STEPS, == *,bench,* ]] && run bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10
+[[ ,$STEPS, == *,bench,* ]] && run bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds ${CPU_SECONDS:-10}
+[[ ,$STEPS, == *,prof,* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-timing
 exit 0
