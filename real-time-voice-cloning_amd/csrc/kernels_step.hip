@@ -33,6 +33,13 @@ struct Tile<CFG1> {
     static constexpr int OPL = 1, NOG = 4;
 };
 
+__device__ __forceinline__ void phase_stamp(uint32_t* ph, int i) {
+    if (ph && threadIdx.x == 0) {
+        const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+        if (wg < kMaxStampWG) ph[8 * wg + i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+}
+
 __device__ __forceinline__ int frame_of(const RowInfo& ri, int t, int hop) {
     const int rel = ri.rel0 + t;
     return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
@@ -146,6 +153,7 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
         if (e < RT * (K / 4)) Xs4[e] = xv[i];
     }
     __syncthreads();
+    phase_stamp(a.phases, 1);
 
     // ---- 3. partial dot products over this thread's k-chunk (fma chain, ascending k) ----
     float acc[OPL][RT];
@@ -170,6 +178,7 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
             }
         }
     }
+    phase_stamp(a.phases, 2);
     __syncthreads();
 
     // ---- 4. partials -> LDS red[og][j][b][kc] (kc contiguous, rows padded) --------------
@@ -179,6 +188,7 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
 #pragma unroll
         for (int b = 0; b < RT; ++b) red[((og * OPL + j) * RT + b) * KCP + kc] = acc[j][b];
     __syncthreads();
+    phase_stamp(a.phases, 3);
 
     // ---- 5. reduce over k-chunks in kc order and apply the epilogue ---------------------
     if (!has_pair) return;
@@ -230,6 +240,7 @@ __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t t_begin = 0;
     if (a.stamps) t_begin = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    phase_stamp(a.phases, 0);
     const int bx = blockIdx.x;
     const int row0 = blockIdx.y * RT;
     int s = 0;
@@ -240,6 +251,10 @@ __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
         case CFG3: seg_tile<K, RT, CFG3>(a, sg, tile, row0, lds); break;
         case CFG2: seg_tile<K, RT, CFG2>(a, sg, tile, row0, lds); break;
         default: seg_tile<K, RT, CFG1>(a, sg, tile, row0, lds); break;
+    }
+    if (a.phases) {
+        __syncthreads();
+        phase_stamp(a.phases, 4);
     }
     if (a.stamps) {
         __syncthreads();
@@ -370,6 +385,33 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
     __shared__ uint32_t words[12];
     const int r = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    phase_stamp(a.phases, 0);
+    // prefetch the GRU1 operands of step t+1 (independent of the sample)
+    constexpr int kMaxUnits = 4;  // H <= 1024
+    const int H = a.H;
+    float g_P[kMaxUnits][3], g_gh[kMaxUnits][3], g_v[kMaxUnits][3], g_h[kMaxUnits],
+        g_c[kMaxUnits], g_w[kMaxUnits];
+    if (a.do_gru) {
+        const int p = a.rows[r].pos0 + a.t + 1;
+        const float* P1 = a.P1 + (size_t)r * 3 * H;
+        const float* gh = a.gh1 + (size_t)r * 3 * H;
+        const float* cI = a.cI + (size_t)p * H;
+#pragma unroll
+        for (int i = 0; i < kMaxUnits; ++i) {
+            const int j = tid + i * kThreads;
+            if (j < H) {
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    g_P[i][g] = P1[g * H + j];
+                    g_gh[i][g] = gh[g * H + j];
+                    g_v[i][g] = a.v[g * H + j];
+                }
+                g_h[i] = a.h1[(size_t)r * H + j];
+                g_c[i] = cI[j];
+                g_w[i] = a.w0[j];
+            }
+        }
+    }
     float x = 0.f;
     if (a.t >= 0) {
         const int n = a.n_classes;
@@ -480,27 +522,31 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
         __syncthreads();
         x = xsh;
     }
+    phase_stamp(a.phases, 1);
     if (!a.do_gru) return;
     // GRU1 of step t+1: gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; xI = cI + w0 x ; x1 = xI + h1
-    const int H = a.H;
-    const int p = a.rows[r].pos0 + a.t + 1;
-    const float* P1 = a.P1 + (size_t)r * 3 * H;
-    const float* gh = a.gh1 + (size_t)r * 3 * H;
-    const float* cI = a.cI + (size_t)p * H;
-    for (int j = tid; j < H; j += kThreads) {
-        const float gi_r = fmaf(a.v[j], x, P1[j]);
-        const float gi_z = fmaf(a.v[H + j], x, P1[H + j]);
-        const float gi_n = fmaf(a.v[2 * H + j], x, P1[2 * H + j]);
-        const float hp = a.h1[(size_t)r * H + j];
-        const float hn = gru_cell(gi_r, gi_z, gi_n, gh[j], gh[H + j], gh[2 * H + j], hp);
-        const float xI = fmaf(a.w0[j], x, cI[j]);
-        a.h1[(size_t)r * H + j] = hn;
-        a.x1[(size_t)r * H + j] = add_nc(xI, hn);
+#pragma unroll
+    for (int i = 0; i < kMaxUnits; ++i) {
+        const int j = tid + i * kThreads;
+        if (j < H) {
+            const float gi_r = fmaf(g_v[i][0], x, g_P[i][0]);
+            const float gi_z = fmaf(g_v[i][1], x, g_P[i][1]);
+            const float gi_n = fmaf(g_v[i][2], x, g_P[i][2]);
+            const float hn = gru_cell(gi_r, gi_z, gi_n, g_gh[i][0], g_gh[i][1], g_gh[i][2], g_h[i]);
+            const float xI = fmaf(g_w[i], x, g_c[i]);
+            a.h1[(size_t)r * H + j] = hn;
+            a.x1[(size_t)r * H + j] = add_nc(xI, hn);
+        }
+    }
+    if (a.phases) {
+        __syncthreads();
+        phase_stamp(a.phases, 2);
     }
 }
 
 hipError_t launch_sample(const SampleArgs& a, hipStream_t s) {
     if (a.mode == 0 && a.n_classes > kMaxClassesPerThread * kThreads) return hipErrorInvalidValue;
+    if (a.H > 4 * kThreads) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_sample, dim3(a.nrows), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }

@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -162,6 +163,8 @@ struct wrnn_handle {
     // ---- call state
     int last_B = 0, last_S = 0, last_L0 = 0, last_T0 = 0;
     bool timing = false;
+    int phase_step = -1;  // diagnostic (env WRNN_PHASE_STEP): per-phase stamps of one step
+    DevBuf phases;
     std::vector<double> stage_avg_us;
     std::vector<int> stage_launches;
     int nrt = 1, RT = 4;
@@ -760,6 +763,9 @@ int build_stage_args(wrnn_handle* h, int si, int t, int S, bool timing, StageArg
     if (timing && t >= 0 && t % kStampEvery == 0)
         a.stamps = (uint32_t*)ws.stamps.p +
                    ((size_t)(t / kStampEvery) * h->stages.size() + si) * kMaxStampWG * 2;
+    a.phases = nullptr;
+    if (t >= 0 && t == h->phase_step && h->phases.p)
+        a.phases = (uint32_t*)h->phases.p + (size_t)si * kMaxStampWG * 8;
     int ns = 0, tile = 0;
     for (size_t k = 0; k < sd.segs.size(); ++k) {
         const SegDesc& d = sd.segs[k];
@@ -835,8 +841,49 @@ int launch_step(wrnn_handle* h, int t, int S, bool timing) {
     sa.rows = (const RowInfo*)h->ws.rows.p;
     sa.k0 = (uint32_t)(h->seed & 0xffffffffu);
     sa.k1 = (uint32_t)(h->seed >> 32);
+    sa.phases = nullptr;
+    if (t == h->phase_step && h->phases.p)
+        sa.phases = (uint32_t*)h->phases.p + h->stages.size() * kMaxStampWG * 8;
     HIPC(launch_sample(sa, st));
     return WRNN_OK;
+}
+
+void phase_report(wrnn_handle* h) {
+    const int ns = (int)h->stages.size();
+    std::vector<uint32_t> ph((size_t)(ns + 1) * kMaxStampWG * 8);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return;
+    if (hipMemcpy(ph.data(), h->phases.p, ph.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+    const int t = h->phase_step;
+    for (int s = 0; s <= ns; ++s) {
+        int nwg, nph;
+        if (s < ns) {
+            StageArgs a;
+            int K;
+            if (build_stage_args(h, s, t, h->last_S, false, &a, &K)) return;
+            nwg = std::min(kMaxStampWG, a.tile_start[a.nseg] * h->nrt);
+            nph = 5;
+        } else {
+            nwg = h->last_B;
+            nph = 3;
+        }
+        const uint32_t* p = ph.data() + (size_t)s * kMaxStampWG * 8;
+        long long t0 = 0;
+        bool first = true;
+        for (int w = 0; w < nwg; ++w) {
+            const long long v = (long long)p[8 * w];
+            if (first || v < t0) t0 = v;
+            first = false;
+        }
+        std::fprintf(stderr, "[wrnn phases] step %d %-6s wg=%4d", t,
+                     s < ns ? h->stages[s].name.c_str() : "sample", nwg);
+        for (int i = 0; i < nph; ++i) {
+            std::vector<double> d;
+            for (int w = 0; w < nwg; ++w) d.push_back(((long long)p[8 * w + i] - t0) * 0.01);
+            std::sort(d.begin(), d.end());
+            std::fprintf(stderr, "  p%d med %.2f max %.2f", i, d[d.size() / 2], d.back());
+        }
+        std::fprintf(stderr, " (us)\n");
+    }
 }
 
 // A noise-seed-dependent kernel argument (MOL Philox key) is baked into captured graphs, so the
@@ -844,7 +891,8 @@ int launch_step(wrnn_handle* h, int t, int S, bool timing) {
 int run_chunk(wrnn_handle* h, int t0, int len, int S) {
     const bool last = t0 + len >= S;
     const int key_S = last ? S : -1;
-    auto key = std::make_tuple(t0, len, key_S, h->last_B, h->timing ? 1 : 0,
+    auto key = std::make_tuple(t0, len, key_S, h->last_B,
+                               (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1),
                                h->cfg.mode == WRNN_MODE_MOL ? h->seed : (uint64_t)0);
     auto it = h->graphs.find(key);
     if (it == h->graphs.end()) {
@@ -951,6 +999,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                               (uint32_t)(h->seed & 0xffffffffu), (uint32_t)(h->seed >> 32),
                               h->stream));
     HIPC(prepare_stage(h->stages[0].K, h->RT));
+    {
+        const char* env = std::getenv("WRNN_PHASE_STEP");
+        h->phase_step = env ? std::atoi(env) : -1;
+        if (h->phase_step >= S) h->phase_step = S - 1;
+        if (h->phase_step >= 0 && !h->phases.p)
+            CHECK(h->phases.alloc((h->stages.size() + 1) * kMaxStampWG * 8 * sizeof(uint32_t)));
+    }
     // initial state: h = 0, gh = b_hh, then P1(0) and GRU1 of step 0
     const int ngru = h->n_gru;
     for (int g = 0; g < ngru; ++g) {
@@ -1051,6 +1106,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     }
     if (seq_len) *seq_len = S;
     h->stream_ctr += (uint32_t)n_utts;
+    if (h->phase_step >= 0) phase_report(h);
     return WRNN_OK;
 }
 

@@ -63,6 +63,7 @@ struct StageArgs {
     const RowInfo* rows;
     uint32_t* stamps;   // optional: workgroup w stores [2w] = start, [2w+1] = end
                         // (low 32 bits of s_memrealtime, 100 MHz) -- no atomics
+    uint32_t* phases;   // optional diagnostic: workgroup w stores 6 stamps at [8w + i]
 };
 
 constexpr int kMaxStampWG = 2048;  // workgroups recorded per timed launch
@@ -85,6 +86,7 @@ struct SampleArgs {
     const float* w0;       // [H] = I.weight[:, 0]
     const RowInfo* rows;
     uint32_t k0, k1;       // Philox key (MOL draws in-kernel)
+    uint32_t* phases;      // optional diagnostic: workgroup w stores 6 stamps at [8w + i]
 };
 
 // ---------------------------------------------------------------------------------------
