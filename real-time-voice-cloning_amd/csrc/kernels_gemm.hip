@@ -18,9 +18,10 @@ __device__ __forceinline__ float load_a(const GemmA& a, int m, int k) {
         case 0:
             return a.p[(size_t)m * a.ld + k];
         case 1: {  // cI: [mel_up(p) (n_mel) | aux(p // hop)[r_off : r_off + n_aux]]
-            if (m >= a.L) return 0.f;
-            if (k < a.n_mel) return a.mel[(size_t)k * a.ldm + m];
-            return a.R[(size_t)(a.r_off + k - a.n_mel) * a.ldr + m / a.hop];
+            const int p = (m % a.Bu) * a.tpo + m / a.Bu;  // fold_with_overlap position
+            if (p >= a.L) return 0.f;                      // zero tail pad
+            if (k < a.n_mel) return a.mel[(size_t)k * a.ldm + p];
+            return a.R[(size_t)(a.r_off + k - a.n_mel) * a.ldr + p / a.hop];
         }
         default: {  // frame-A: slot 0 is the zero frame; slot f+1 = frame f
             if (m == 0) return 0.f;
@@ -46,6 +47,11 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
         case 1:
             v = acc + e.bias[m];
             break;
+        case 3: {
+            const size_t row = (size_t)(m / e.Bu) * e.Btot + e.row0 + m % e.Bu;
+            e.D[row * e.ld + n] = acc + e.bias[n];
+            return;
+        }
         default: {
             // eval BatchNorm as torch CPU: x * (w / sqrt(var + eps)) + (b - mean * alpha)
             v = fmaf(acc, e.alpha[m], e.beta[m]);

@@ -18,21 +18,6 @@
 
 namespace wrnn {
 
-template <int CFG>
-struct Tile;
-template <>
-struct Tile<CFG3> {
-    static constexpr int OPL = 3, NOG = 4;
-};
-template <>
-struct Tile<CFG2> {
-    static constexpr int OPL = 2, NOG = 8;
-};
-template <>
-struct Tile<CFG1> {
-    static constexpr int OPL = 1, NOG = 4;
-};
-
 __device__ __forceinline__ void phase_stamp(uint32_t* ph, int i) {
     if (ph && threadIdx.x == 0) {
         const int wg = blockIdx.y * gridDim.x + blockIdx.x;
@@ -69,28 +54,30 @@ __device__ __forceinline__ float add_nc(float a, float b) {
     return a + b;
 }
 
-template <int K, int RT, int CFG>
+template <int K, int RT, int NRG, int CFG>
 __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int tile, int row0,
                                          float* lds) {
-    constexpr int OPL = Tile<CFG>::OPL, NOG = Tile<CFG>::NOG;
-    constexpr int KC = kThreads / NOG;
-    constexpr int KR = K / KC;
+    constexpr int OPL = CFG == TILE_GATE ? 3 : 1;
+    constexpr int NOG = kTileNOG;
+    constexpr int KC = kThreads / (NOG * NRG);  // k-chunks
+    constexpr int KR = K / KC;                  // k per thread
+    constexpr int BR = RT / NRG;                // rows per thread
     constexpr int KCP = KC + 4;  // padded reduction row: conflict-free ds_read_b128 per row
     constexpr int NX = (RT * (K / 4) + kThreads - 1) / kThreads;  // X float4 per thread
-    static_assert(KR % 4 == 0, "k-chunk must be a multiple of 4");
+    static_assert(KR % 4 == 0 && KC % 4 == 0 && RT % NRG == 0, "bad tile shape");
     static_assert(NOG * RT <= kThreads, "one epilogue pair per thread");
     const int tid = threadIdx.x;
-    const int og = tid % NOG, kc = tid / NOG;
+    const int og = tid % NOG, rg = (tid / NOG) % NRG, kc = tid / (NOG * NRG);
     const int nrows = a.nrows;
     const int H = sg.H;
     const bool gather = sg.x_pld != 0;
 
     // ---- 1. issue every global load of this tile up front (latency overlaps) ------------
-    // weight tile -> registers; packed [tile][kc][og][j][kk] == [tile][tid][j][kk]
+    // weight tile -> registers; packed [tile][kc][og][j][kk] (row groups share a slice)
     float4 wv[OPL * KR / 4];
     {
         const float4* wp = reinterpret_cast<const float4*>(
-            sg.W + ((size_t)tile * kThreads + tid) * (size_t)(OPL * KR));
+            sg.W + (((size_t)tile * KC + kc) * NOG + og) * (size_t)(OPL * KR));
 #pragma unroll
         for (int i = 0; i < OPL * KR / 4; ++i) wv[i] = wp[i];
     }
@@ -115,33 +102,26 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
     float e_c[OPL], e_gh[3] = {0.f, 0.f, 0.f}, e_h = 0.f, e_x = 0.f;
 #pragma unroll
     for (int j = 0; j < OPL; ++j) e_c[j] = 0.f;
-    int e_u = 0;
+    const int e_o = tile * NOG + pog;  // unit (TILE_GATE) or output (TILE_OUT)
     if (has_pair) {
-        if constexpr (CFG == CFG3) {
-            e_u = tile * NOG + pog;
-            if (e_u < H) {
-                const float* cr = sg.cond;
-                if (sg.c_ld) cr += (size_t)frame_of(a.rows[pr], a.t, a.hop) * (size_t)sg.c_ld;
+        const float* cr = sg.cond;
+        if (sg.c_ld) cr += (size_t)frame_of(a.rows[pr], a.t, a.hop) * (size_t)sg.c_ld;
+        if constexpr (CFG == TILE_GATE) {
+            if (e_o < H) {
 #pragma unroll
-                for (int j = 0; j < 3; ++j) e_c[j] = cr[j * H + e_u];
+                for (int j = 0; j < 3; ++j) e_c[j] = cr[j * H + e_o];
                 if (sg.kind == EPI_GRU) {
                     const float* gh = sg.gh + (size_t)pr * 3 * H;
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) e_gh[j] = gh[j * H + e_u];
-                    e_h = sg.h[(size_t)pr * H + e_u];
+                    for (int j = 0; j < 3; ++j) e_gh[j] = gh[j * H + e_o];
+                    e_h = sg.h[(size_t)pr * H + e_o];
                     long long off = sg.x_off + (long long)pr * sg.x_ld;
                     if (gather) off += (long long)a.rows[pr].pos0 * sg.x_pld;
-                    e_x = sg.X[off + e_u];
+                    e_x = sg.X[off + e_o];
                 }
             }
         } else {
-            const float* cr = sg.cond;
-            if (sg.c_ld) cr += (size_t)frame_of(a.rows[pr], a.t, a.hop) * (size_t)sg.c_ld;
-#pragma unroll
-            for (int j = 0; j < OPL; ++j) {
-                const int o = (tile * NOG + pog) * OPL + j;
-                e_c[j] = o < sg.n_out ? cr[o] : 0.f;
-            }
+            if (e_o < sg.n_out) e_c[0] = cr[e_o];
         }
     }
 
@@ -156,25 +136,26 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
     phase_stamp(a.phases, 1);
 
     // ---- 3. partial dot products over this thread's k-chunk (fma chain, ascending k) ----
-    float acc[OPL][RT];
+    float acc[OPL][BR];
 #pragma unroll
     for (int j = 0; j < OPL; ++j)
 #pragma unroll
-        for (int b = 0; b < RT; ++b) acc[j][b] = 0.f;
+        for (int i = 0; i < BR; ++i) acc[j][i] = 0.f;
 #pragma unroll
-    for (int b = 0; b < RT; ++b) {
+    for (int i = 0; i < BR; ++i) {
+        const int b = rg * BR + i;
 #pragma unroll
         for (int q = 0; q < KR / 4; ++q) {
             const float4 x4 = Xs4[b * (K / 4) + kc * (KR / 4) + q];
 #pragma unroll
             for (int j = 0; j < OPL; ++j) {
                 const float4 w4 = wv[j * (KR / 4) + q];
-                float s = acc[j][b];
+                float s = acc[j][i];
                 s = fmaf(w4.x, x4.x, s);
                 s = fmaf(w4.y, x4.y, s);
                 s = fmaf(w4.z, x4.z, s);
                 s = fmaf(w4.w, x4.w, s);
-                acc[j][b] = s;
+                acc[j][i] = s;
             }
         }
     }
@@ -186,7 +167,8 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
 #pragma unroll
     for (int j = 0; j < OPL; ++j)
 #pragma unroll
-        for (int b = 0; b < RT; ++b) red[((og * OPL + j) * RT + b) * KCP + kc] = acc[j][b];
+        for (int i = 0; i < BR; ++i)
+            red[((og * OPL + j) * RT + rg * BR + i) * KCP + kc] = acc[j][i];
     __syncthreads();
     phase_stamp(a.phases, 3);
 
@@ -207,35 +189,30 @@ __device__ __forceinline__ void seg_tile(const StageArgs& a, const Seg& sg, int 
         }
         s[j] = v;
     }
-    if constexpr (CFG == CFG3) {
-        if (e_u >= H) return;
+    if constexpr (CFG == TILE_GATE) {
+        if (e_o >= H) return;
         if (sg.kind == EPI_GRU) {
             const float gi_r = add_nc(s[0], e_c[0]);
             const float gi_z = add_nc(s[1], e_c[1]);
             const float gi_n = add_nc(s[2], e_c[2]);
             const float hn = gru_cell(gi_r, gi_z, gi_n, e_gh[0], e_gh[1], e_gh[2], e_h);
-            sg.h[(size_t)pr * H + e_u] = hn;
-            sg.xout[(size_t)pr * H + e_u] = add_nc(e_x, hn);
+            sg.h[(size_t)pr * H + e_o] = hn;
+            sg.xout[(size_t)pr * H + e_o] = add_nc(e_x, hn);
         } else {  // EPI_BIAS3
             float* y = sg.Y + (size_t)pr * sg.y_ld;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) y[j * H + e_u] = add_nc(s[j], e_c[j]);
+            for (int j = 0; j < 3; ++j) y[j * H + e_o] = add_nc(s[j], e_c[j]);
         }
     } else {
-        float* y = sg.Y + (size_t)pr * sg.y_ld;
-#pragma unroll
-        for (int j = 0; j < OPL; ++j) {
-            const int o = (tile * NOG + pog) * OPL + j;
-            if (o < sg.n_out) {
-                float v = add_nc(s[j], e_c[j]);
-                if (sg.kind == EPI_COND_RELU) v = v > 0.f ? v : 0.f;
-                y[o] = v;
-            }
+        if (e_o < sg.n_out) {
+            float v = add_nc(s[0], e_c[0]);
+            if (sg.kind == EPI_COND_RELU) v = v > 0.f ? v : 0.f;
+            sg.Y[(size_t)pr * sg.y_ld + e_o] = v;
         }
     }
 }
 
-template <int K, int RT>
+template <int K, int RT, int NRG>
 __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t t_begin = 0;
@@ -247,11 +224,10 @@ __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
     while (s + 1 < a.nseg && bx >= a.tile_start[s + 1]) ++s;
     const Seg& sg = a.seg[s];
     const int tile = bx - a.tile_start[s];
-    switch (sg.cfg) {
-        case CFG3: seg_tile<K, RT, CFG3>(a, sg, tile, row0, lds); break;
-        case CFG2: seg_tile<K, RT, CFG2>(a, sg, tile, row0, lds); break;
-        default: seg_tile<K, RT, CFG1>(a, sg, tile, row0, lds); break;
-    }
+    if (sg.cfg == TILE_GATE)
+        seg_tile<K, RT, NRG, TILE_GATE>(a, sg, tile, row0, lds);
+    else
+        seg_tile<K, RT, NRG, TILE_OUT>(a, sg, tile, row0, lds);
     if (a.phases) {
         __syncthreads();
         phase_stamp(a.phases, 4);
@@ -266,136 +242,178 @@ __global__ __launch_bounds__(kThreads) void k_stage(StageArgs a) {
     }
 }
 
-template <int K, int RT>
+template <int K, int RT, int NRG>
 static size_t stage_lds_bytes() {
     const size_t xs = (size_t)RT * K * sizeof(float);
-    const size_t red = (size_t)4 * 3 * RT * (64 + 4) * sizeof(float);  // NOG*OPL*RT*KCP max
+    const size_t kcp = kThreads / (kTileNOG * NRG) + 4;
+    const size_t red = (size_t)kTileNOG * 3 * RT * kcp * sizeof(float);
     return xs > red ? xs : red;
 }
 
-template <int K, int RT>
+template <int K, int RT, int NRG>
 static hipError_t prepare_stage_t() {
-    return hipFuncSetAttribute((const void*)k_stage<K, RT>,
+    return hipFuncSetAttribute((const void*)k_stage<K, RT, NRG>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)stage_lds_bytes<K, RT>());
+                               (int)stage_lds_bytes<K, RT, NRG>());
 }
 
-template <int K, int RT>
+template <int K, int RT, int NRG>
 static hipError_t launch_stage_t(const StageArgs& a, int n_row_tiles, hipStream_t s) {
     const int n_tiles = a.tile_start[a.nseg];
-    const size_t lds = stage_lds_bytes<K, RT>();
-    hipLaunchKernelGGL((k_stage<K, RT>), dim3(n_tiles, n_row_tiles), dim3(kThreads), lds, s, a);
+    const size_t lds = stage_lds_bytes<K, RT, NRG>();
+    hipLaunchKernelGGL((k_stage<K, RT, NRG>), dim3(n_tiles, n_row_tiles), dim3(kThreads), lds, s,
+                       a);
     return hipGetLastError();
 }
 
-#define WRNN_RT_CASES(K)                                                  \
-    switch (RT) {                                                         \
-        case 4: return launch_stage_t<K, 4>(a, n_row_tiles, s);           \
-        case 8: return launch_stage_t<K, 8>(a, n_row_tiles, s);           \
-        case 12: return launch_stage_t<K, 12>(a, n_row_tiles, s);         \
-        case 16: return launch_stage_t<K, 16>(a, n_row_tiles, s);         \
-        case 20: return launch_stage_t<K, 20>(a, n_row_tiles, s);         \
-        case 24: return launch_stage_t<K, 24>(a, n_row_tiles, s);         \
-        case 32: return launch_stage_t<K, 32>(a, n_row_tiles, s);         \
-        default: return hipErrorInvalidValue;                             \
+template <int K, int RT>
+static hipError_t dispatch_nrg(bool prep, const StageArgs* a, int NRG, int nrt, hipStream_t s) {
+    switch (NRG) {
+        case 1: return prep ? prepare_stage_t<K, RT, 1>() : launch_stage_t<K, RT, 1>(*a, nrt, s);
+        case 2: return prep ? prepare_stage_t<K, RT, 2>() : launch_stage_t<K, RT, 2>(*a, nrt, s);
+        case 4: return prep ? prepare_stage_t<K, RT, 4>() : launch_stage_t<K, RT, 4>(*a, nrt, s);
+        default: return hipErrorInvalidValue;
     }
+}
 
-#define WRNN_RT_PREP(K)                               \
-    switch (RT) {                                     \
-        case 4: return prepare_stage_t<K, 4>();       \
-        case 8: return prepare_stage_t<K, 8>();       \
-        case 12: return prepare_stage_t<K, 12>();     \
-        case 16: return prepare_stage_t<K, 16>();     \
-        case 20: return prepare_stage_t<K, 20>();     \
-        case 24: return prepare_stage_t<K, 24>();     \
-        case 32: return prepare_stage_t<K, 32>();     \
-        default: return hipErrorInvalidValue;         \
+template <int K>
+static hipError_t dispatch_rt(bool prep, const StageArgs* a, int RT, int NRG, int nrt,
+                              hipStream_t s) {
+    switch (RT) {
+        case 4: return dispatch_nrg<K, 4>(prep, a, NRG, nrt, s);
+        case 8: return dispatch_nrg<K, 8>(prep, a, NRG, nrt, s);
+        case 12: return dispatch_nrg<K, 12>(prep, a, NRG, nrt, s);
+        case 16: return dispatch_nrg<K, 16>(prep, a, NRG, nrt, s);
+        case 20: return dispatch_nrg<K, 20>(prep, a, NRG, nrt, s);
+        case 24: return dispatch_nrg<K, 24>(prep, a, NRG, nrt, s);
+        case 32: return dispatch_nrg<K, 32>(prep, a, NRG, nrt, s);
+        default: return hipErrorInvalidValue;
     }
+}
 
-hipError_t prepare_stage(int K, int RT) {
-    if (K == 512) {
-        WRNN_RT_PREP(512)
-    } else if (K == 256) {
-        WRNN_RT_PREP(256)
-    }
+hipError_t prepare_stage(int K, int RT, int NRG) {
+    if (K == 512) return dispatch_rt<512>(true, nullptr, RT, NRG, 0, nullptr);
+    if (K == 256) return dispatch_rt<256>(true, nullptr, RT, NRG, 0, nullptr);
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_stage(const StageArgs& a, int K, int RT, int n_row_tiles, hipStream_t s) {
-    if (K == 512) {
-        WRNN_RT_CASES(512)
-    } else if (K == 256) {
-        WRNN_RT_CASES(256)
-    }
+hipError_t launch_stage(const StageArgs& a, int K, int RT, int NRG, int n_row_tiles,
+                        hipStream_t s) {
+    if (K == 512) return dispatch_rt<512>(false, &a, RT, NRG, n_row_tiles, s);
+    if (K == 256) return dispatch_rt<256>(false, &a, RT, NRG, n_row_tiles, s);
     return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------------------
 // Sampling + GRU1 of the next step (one workgroup per fold row).
+// Wave reductions use DPP (quad_perm / row_ror inside 16-lane rows, readlane across rows);
+// the order of every reduction is fixed, so results are run-to-run deterministic.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ void wave_argmax(float& v, int& i) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float v2 = __shfl_xor(v, o, 64);
-        const int i2 = __shfl_xor(i, o, 64);
-        if (v2 > v || (v2 == v && i2 < i)) {
-            v = v2;
-            i = i2;
-        }
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppRor4 = 0x124, kDppRor8 = 0x128;
+
+__device__ __forceinline__ float wave_max_all(float v) {
+    v = fmaxf(v, dppf<kDppXor1>(v));
+    v = fmaxf(v, dppf<kDppXor2>(v));
+    v = fmaxf(v, dppf<kDppRor4>(v));
+    v = fmaxf(v, dppf<kDppRor8>(v));
+    return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
+}
+__device__ __forceinline__ float wave_sum_all(float v) {
+    v += dppf<kDppXor1>(v);
+    v += dppf<kDppXor2>(v);
+    v += dppf<kDppRor4>(v);
+    v += dppf<kDppRor8>(v);
+    return ((lanef(v, 0) + lanef(v, 16)) + lanef(v, 32)) + lanef(v, 48);
+}
+__device__ __forceinline__ void amax_step(float& v, int& i, float v2, int i2) {
+    if (v2 > v || (v2 == v && i2 < i)) {
+        v = v2;
+        i = i2;
     }
 }
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp(float& v, int& i) {
+    amax_step(v, i, dppf<CTRL>(v), dppi<CTRL>(i));
+}
+__device__ __forceinline__ void wave_argmax_all(float& v, int& i) {
+    amax_dpp<kDppXor1>(v, i);
+    amax_dpp<kDppXor2>(v, i);
+    amax_dpp<kDppRor4>(v, i);
+    amax_dpp<kDppRor8>(v, i);
+    float bv = lanef(v, 0);
+    int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int l = 16; l < 64; l += 16)
+        amax_step(bv, bi, lanef(v, l), __builtin_amdgcn_readlane(i, l));
+    v = bv;
+    i = bi;
+}
 
-__device__ float block_max(float v, float* sh) {
-    v = wave_max(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
+constexpr int kWaves = kThreads / 64;
+
+__device__ __forceinline__ float block_max(float v, float* sh) {
+    v = wave_max_all(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
     float r = sh[0];
-    for (int i = 1; i < kThreads / 64; ++i) r = fmaxf(r, sh[i]);
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) r = fmaxf(r, sh[w]);
+    __syncthreads();
     return r;
 }
-__device__ float block_sum(float v, float* sh) {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+    v = wave_sum_all(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
     float r = sh[0];
-    for (int i = 1; i < kThreads / 64; ++i) r += sh[i];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) r += sh[w];
+    __syncthreads();
     return r;
 }
 
 constexpr int kMaxClassesPerThread = 16;  // n_classes <= 4096 (bits <= 12)
+constexpr int kMaxUnits = 4;              // H <= 1024
 
 __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
-    __shared__ float shf[8];
-    __shared__ int shi[8];
+    __shared__ float shf[kWaves];
+    __shared__ int shi[kWaves];
     __shared__ float xsh;
     __shared__ uint32_t words[12];
     const int r = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     phase_stamp(a.phases, 0);
-    // prefetch the GRU1 operands of step t+1 (independent of the sample)
-    constexpr int kMaxUnits = 4;  // H <= 1024
     const int H = a.H;
+    const int n = a.n_classes;
+    const RowInfo ri = a.rows[r];
+    // 1. loads that do not depend on the sample: logits, GRU1 operands of step t+1
+    float l[kMaxClassesPerThread];
+    if (a.t >= 0 && a.mode == 0) {
+        const float* lg = a.logits + (size_t)r * n;
+#pragma unroll
+        for (int i = 0; i < kMaxClassesPerThread; ++i) {
+            const int k = tid + i * kThreads;
+            l[i] = k < n ? lg[k] : -INFINITY;
+        }
+    }
     float g_P[kMaxUnits][3], g_gh[kMaxUnits][3], g_v[kMaxUnits][3], g_h[kMaxUnits],
         g_c[kMaxUnits], g_w[kMaxUnits];
     if (a.do_gru) {
-        const int p = a.rows[r].pos0 + a.t + 1;
+        // folded conditioning: cI rows of step t+1 are contiguous ([t][row][H])
         const float* P1 = a.P1 + (size_t)r * 3 * H;
         const float* gh = a.gh1 + (size_t)r * 3 * H;
-        const float* cI = a.cI + (size_t)p * H;
+        const float* cI = a.cI + ((size_t)(a.t + 1) * a.nrows + r) * H;
 #pragma unroll
         for (int i = 0; i < kMaxUnits; ++i) {
             const int j = tid + i * kThreads;
@@ -414,19 +432,30 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
     }
     float x = 0.f;
     if (a.t >= 0) {
-        const int n = a.n_classes;
-        const float* lg = a.logits + (size_t)r * n;
         if (a.mode == 0) {
-            const float* qn = a.noise + ((size_t)a.t * a.nrows + r) * n;
-            float l[kMaxClassesPerThread], q[kMaxClassesPerThread];
+            // 2. Exp(1) noise of this row-step, computed while the logits are in flight
+            float q[kMaxClassesPerThread];
+#pragma unroll
+            for (int i = 0; i < kMaxClassesPerThread; i += 4) {
+                // classes k = tid + (i..i+3)*256 come from 4 different Philox blocks
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = tid + (i + u) * kThreads;
+                    q[i + u] = 1.f;
+                    if (k < n) {
+                        const U4 o = philox4x32_10((uint32_t)(k >> 2), (uint32_t)a.t,
+                                                   (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+                        const uint32_t w = (k & 3) == 0 ? o.x : (k & 3) == 1 ? o.y
+                                         : (k & 3) == 2 ? o.z : o.w;
+                        q[i + u] = exp1_from_u32(w);
+                    }
+                }
+            }
+            // 3. torch softmax + Categorical renormalisation + multinomial fast path:
+            //    k* = argmax((p / sum p) / q)
             float m = -INFINITY;
 #pragma unroll
-            for (int i = 0; i < kMaxClassesPerThread; ++i) {
-                const int k = tid + i * kThreads;
-                l[i] = k < n ? lg[k] : -INFINITY;
-                q[i] = k < n ? qn[k] : 1.f;
-                m = fmaxf(m, l[i]);
-            }
+            for (int i = 0; i < kMaxClassesPerThread; ++i) m = fmaxf(m, l[i]);
             m = block_max(m, shf);
             float e[kMaxClassesPerThread];
             float se = 0.f;
@@ -440,10 +469,10 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
             float sp = 0.f;
 #pragma unroll
             for (int i = 0; i < kMaxClassesPerThread; ++i) {
-                e[i] = e[i] / se;  // softmax
+                e[i] = e[i] / se;
                 sp += e[i];
             }
-            sp = block_sum(sp, shf);  // Categorical re-normalisation
+            sp = block_sum(sp, shf);
             float best = -INFINITY;
             int bi = 0x7fffffff;
 #pragma unroll
@@ -451,39 +480,30 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
                 const int k = tid + i * kThreads;
                 if (k < n) {
                     const float ratio = (e[i] / sp) / q[i];
-                    if (ratio > best || (ratio == best && k < bi)) {
-                        best = ratio;
-                        bi = k;
-                    }
+                    amax_step(best, bi, ratio, k);
                 }
             }
-            wave_argmax(best, bi);
-            __syncthreads();
+            wave_argmax_all(best, bi);
             if (lane == 0) {
                 shf[wv] = best;
                 shi[wv] = bi;
             }
             __syncthreads();
-            if (tid == 0) {
-                float bv = shf[0];
-                int bk = shi[0];
-                for (int i = 1; i < kThreads / 64; ++i)
-                    if (shf[i] > bv || (shf[i] == bv && shi[i] < bk)) {
-                        bv = shf[i];
-                        bk = shi[i];
-                    }
-                float xv;
-                {
+            float bv = shf[0];
+            int bk = shi[0];
+#pragma unroll
+            for (int w = 1; w < kWaves; ++w) amax_step(bv, bk, shf[w], shi[w]);
+            {
 #pragma clang fp contract(off)
-                    xv = (2.0f * (float)bk) / (float)(n - 1) - 1.0f;
-                }
+                x = (2.0f * (float)bk) / (float)(n - 1) - 1.0f;
+            }
+            if (tid == 0) {
                 a.labels[(size_t)r * a.S + a.t] = (int16_t)bk;
-                a.samples[(size_t)r * a.S + a.t] = xv;
-                xsh = xv;
+                a.samples[(size_t)r * a.S + a.t] = x;
             }
         } else {
             // MOL: vocoder/distribution.py:104-140 with the Philox draws
-            const RowInfo ri = a.rows[r];
+            const float* lg = a.logits + (size_t)r * n;
             if (tid < 3) {
                 const U4 o = philox4x32_10(kMolDomain | (uint32_t)tid, (uint32_t)a.t,
                                            (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
@@ -502,7 +522,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
                     v = lg[lane] - logf(-logf(u1));
                     idx = lane;
                 }
-                wave_argmax(v, idx);
+                wave_argmax_all(v, idx);
                 if (lane == 0) {
 #pragma clang fp contract(off)
                     const float u2 = mol_uniform_from_u32(words[10]);
@@ -518,13 +538,13 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
                     xsh = xv;
                 }
             }
+            __syncthreads();
+            x = xsh;
         }
-        __syncthreads();
-        x = xsh;
     }
     phase_stamp(a.phases, 1);
     if (!a.do_gru) return;
-    // GRU1 of step t+1: gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; xI = cI + w0 x ; x1 = xI + h1
+    // 4. GRU1 of step t+1: gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; xI = cI + w0 x
 #pragma unroll
     for (int i = 0; i < kMaxUnits; ++i) {
         const int j = tid + i * kThreads;
@@ -546,7 +566,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
 
 hipError_t launch_sample(const SampleArgs& a, hipStream_t s) {
     if (a.mode == 0 && a.n_classes > kMaxClassesPerThread * kThreads) return hipErrorInvalidValue;
-    if (a.H > 4 * kThreads) return hipErrorInvalidValue;
+    if (a.H > kMaxUnits * kThreads) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_sample, dim3(a.nrows), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }

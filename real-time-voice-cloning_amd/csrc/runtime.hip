@@ -111,9 +111,6 @@ struct StageDesc {
     bool next_step_only;  // segment list index 1.. may be dropped at the last step (P1)
 };
 
-int tile_outputs(int cfg) { return cfg == CFG3 ? 4 : (cfg == CFG2 ? 16 : 4); }
-int tile_opl(int cfg) { return cfg == CFG3 ? 3 : (cfg == CFG2 ? 2 : 1); }
-int tile_nog(int cfg) { return cfg == CFG3 ? 4 : (cfg == CFG2 ? 8 : 4); }
 
 }  // namespace
 
@@ -168,6 +165,7 @@ struct wrnn_handle {
     std::vector<double> stage_avg_us;
     std::vector<int> stage_launches;
     int nrt = 1, RT = 4;
+    int nrg = 2;  // row groups per stage tile (env WRNN_NRG: 1, 2 or 4)
     std::vector<RowInfo> rows_host;
 
     ~wrnn_handle() {
@@ -260,36 +258,32 @@ const float* upload(wrnn_handle* h, const std::vector<float>& v, int* rc) {
 }
 
 // Pack rows of a PyTorch (n_rows, ld) weight for the stage tile scheme of kernels_step.hip:
-// [tile][kc][og][j][kk]; CFG3 tiles are unit-interleaved (j = gate r/z/n of unit u).
+// [tile][kc][og][j][kk] with KC = 256 / (NOG * NRG); TILE_GATE tiles are unit-interleaved
+// (j = gate r/z/n of unit u, rows j*H + u of the PyTorch gate-major weight).
 PackedSeg pack_segment(wrnn_handle* h, const std::vector<float>& W, int n_out, int ld, int col0,
                        int K, int cfg, int Hg, int* rc) {
     PackedSeg ps;
     ps.cfg = cfg;
     ps.K = K;
     ps.n_out = n_out;
-    const int OPL = tile_opl(cfg), NOG = tile_nog(cfg);
-    const int KC = kThreads / NOG, KR = K / KC;
-    if (cfg == CFG3) {
-        ps.n_tiles = (Hg + NOG - 1) / NOG;
-    } else {
-        const int OT = OPL * NOG;
-        ps.n_tiles = (n_out + OT - 1) / OT;
-    }
-    std::vector<float> out((size_t)ps.n_tiles * kThreads * OPL * KR, 0.f);
+    const int OPL = tile_opl(cfg), NOG = kTileNOG;
+    const int KC = kThreads / (NOG * h->nrg), KR = K / KC;
+    ps.n_tiles = cfg == TILE_GATE ? (Hg + NOG - 1) / NOG : (n_out + NOG - 1) / NOG;
+    std::vector<float> out((size_t)ps.n_tiles * KC * NOG * OPL * KR, 0.f);
     size_t idx = 0;
     for (int tile = 0; tile < ps.n_tiles; ++tile)
-        for (int tid = 0; tid < kThreads; ++tid) {
-            const int og = tid % NOG, kc = tid / NOG;
+        for (int kc = 0; kc < KC; ++kc)
+            for (int og = 0; og < NOG; ++og) {
             for (int j = 0; j < OPL; ++j)
                 for (int kk = 0; kk < KR; ++kk, ++idx) {
                     int o;
                     bool valid;
-                    if (cfg == CFG3) {
+                    if (cfg == TILE_GATE) {
                         const int u = tile * NOG + og;
                         valid = u < Hg;
                         o = j * Hg + u;
                     } else {
-                        o = (tile * NOG + og) * OPL + j;
+                        o = tile * NOG + og;
                         valid = o < n_out;
                     }
                     const int k = kc * KR + kk;
@@ -315,6 +309,11 @@ std::vector<float> transpose_cols(const std::vector<float>& W, int rows, int ld,
 }
 
 int do_finalize(wrnn_handle* h) {
+    if (const char* env = std::getenv("WRNN_NRG")) {
+        const int v = std::atoi(env);
+        if (v != 1 && v != 2 && v != 4) return fail(WRNN_ERR_INVALID, "WRNN_NRG must be 1, 2 or 4");
+        h->nrg = v;
+    }
     for (auto& kv : h->expected)
         if (!h->host.count(kv.first))
             return fail(WRNN_ERR_INVALID, "missing state-dict tensor '" + kv.first + "'");
@@ -423,7 +422,7 @@ int do_finalize(wrnn_handle* h) {
     auto seg_gru = [&](const std::string& gname, int col0_ld, int x, int gh, int hh, int xout,
                        const float* cond, int fc) {
         SegDesc s{};
-        s.w = pack_segment(h, T[gname + ".weight_ih_l0"], 3 * H, col0_ld, 0, K, CFG3, H, &rc);
+        s.w = pack_segment(h, T[gname + ".weight_ih_l0"], 3 * H, col0_ld, 0, K, TILE_GATE, H, &rc);
         s.kind = EPI_GRU;
         s.x = x;
         s.y = SL_NONE;
@@ -437,7 +436,7 @@ int do_finalize(wrnn_handle* h) {
     };
     auto seg_hh = [&](const std::string& gname, int hsl, int ghsl) {
         SegDesc s{};
-        s.w = pack_segment(h, T[gname + ".weight_hh_l0"], 3 * H, H, 0, K, CFG3, H, &rc);
+        s.w = pack_segment(h, T[gname + ".weight_hh_l0"], 3 * H, H, 0, K, TILE_GATE, H, &rc);
         s.kind = EPI_BIAS3;
         s.x = hsl;
         s.y = ghsl;
@@ -449,7 +448,7 @@ int do_finalize(wrnn_handle* h) {
     };
     auto seg_p1 = [&]() {
         SegDesc s{};
-        s.w = pack_segment(h, T["rnn1.weight_ih_l0"], 3 * H, H, 0, K, CFG3, H, &rc);
+        s.w = pack_segment(h, T["rnn1.weight_ih_l0"], 3 * H, H, 0, K, TILE_GATE, H, &rc);
         s.kind = EPI_BIAS3;
         s.x = SL_CI;
         s.y = SL_P1;
@@ -462,7 +461,7 @@ int do_finalize(wrnn_handle* h) {
     auto seg_fc = [&](const std::string& nm, int n_out, int ld, int x, int y, bool relu,
                       const float* cond, int fc) {
         SegDesc s{};
-        s.w = pack_segment(h, T[nm + ".weight"], n_out, ld, 0, K, CFG1, 0, &rc);
+        s.w = pack_segment(h, T[nm + ".weight"], n_out, ld, 0, K, TILE_OUT, 0, &rc);
         s.kind = relu ? EPI_COND_RELU : EPI_COND;
         s.x = x;
         s.y = y;
@@ -574,9 +573,7 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
     ws.rows.release();
     CHECK(ws.labels.alloc((size_t)nB * nS * sizeof(int16_t)));
     CHECK(ws.samples.alloc((size_t)nB * nS * sizeof(float)));
-    if (h->cfg.mode == WRNN_MODE_RAW)
-        CHECK(ws.noise.alloc((size_t)nS * nB * h->n_classes * sizeof(float)));
-    CHECK(ws.cI.alloc((size_t)nP * h->H * sizeof(float)));
+    CHECK(ws.cI.alloc((size_t)nS * nB * h->H * sizeof(float)));  // folded [t][row][H]
     CHECK(ws.fcond.alloc((size_t)nF * h->cond_width * sizeof(float)));
     CHECK(ws.rows.alloc((size_t)nB * sizeof(RowInfo)));
     // upsample scratch for one utterance of <= nT frames
@@ -604,7 +601,8 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
 }
 
 // ---- upsample network + conditioning for one utterance --------------------------------
-int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Lpad, int pbase, int fbase) {
+int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
+                 int row0, int fbase) {
     auto& ws = h->ws;
     hipStream_t st = h->stream;
     const int C = h->C, R = h->R, H = h->H;
@@ -705,7 +703,8 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Lpad, int pbase,
             W_in = W_out;
         }
     }
-    // cI[p] = I.weight[:,1:] . [mel_up(p), aux(p)[:A-1]] + I.bias for p in [0, Lpad)
+    // cI(t, row) = I.weight[:,1:] . [mel_up(p), aux(p)[:A-1]] + I.bias, p = fold*tpo + t,
+    // written in the folded step-major layout [t][row][H] the recurrence reads contiguously
     {
         GemmA a4{};
         GemmB b4{};
@@ -720,14 +719,19 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Lpad, int pbase,
         a4.ldr = T;
         a4.r_off = 0;
         a4.n_aux = h->A - 1;
+        a4.Bu = Bu;
+        a4.tpo = tpo;
         b4.kind = 0;
         b4.p = h->WIT;
         b4.ld = H;
-        e4.kind = 0;
-        e4.D = ws.cI.f() + (size_t)pbase * H;
+        e4.kind = 3;
+        e4.D = ws.cI.f();
         e4.ld = H;
         e4.bias = h->bI;
-        HIPC(launch_gemm(Lpad, H, h->KI, a4, b4, e4, st));
+        e4.Bu = Bu;
+        e4.Btot = Btot;
+        e4.row0 = row0;
+        HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
     }
     // per-frame aux conditioning, slot 0 = zero frame
     for (const auto& ac : h->auxc) {
@@ -779,9 +783,9 @@ int build_stage_args(wrnn_handle* h, int si, int t, int S, bool timing, StageArg
         g.H = h->H;
         if (d.x == SL_CI) {
             g.X = ws.cI.f();
-            g.x_off = (long long)(t + 1) * h->H;
-            g.x_ld = 0;
-            g.x_pld = h->H;
+            g.x_off = (long long)(t + 1) * h->last_B * h->H;
+            g.x_ld = h->H;
+            g.x_pld = 0;
         } else {
             g.X = h->slot(d.x);
             g.x_off = 0;
@@ -817,7 +821,7 @@ int launch_step(wrnn_handle* h, int t, int S, bool timing) {
         StageArgs a;
         int K;
         CHECK(build_stage_args(h, (int)si, t, S, timing, &a, &K));
-        HIPC(launch_stage(a, K, h->RT, h->nrt, st));
+        HIPC(launch_stage(a, K, h->RT, h->nrg, h->nrt, st));
     }
     SampleArgs sa{};
     sa.t = t;
@@ -827,7 +831,7 @@ int launch_step(wrnn_handle* h, int t, int S, bool timing) {
     sa.mode = h->cfg.mode;
     sa.H = h->H;
     sa.logits = h->slot(SL_LOG);
-    sa.noise = h->ws.noise.f();
+    sa.noise = nullptr;
     sa.samples = h->ws.samples.f();
     sa.labels = (int16_t*)h->ws.labels.p;
     sa.do_gru = t + 1 < S;
@@ -992,13 +996,9 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                         hipMemcpyHostToDevice, h->stream));
     // upsample + conditioning per utterance
     for (int u = 0; u < n_utts; ++u)
-        CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].Lpad, plan[u].pbase, plan[u].fbase));
-    // noise
-    if (h->cfg.mode == WRNN_MODE_RAW)
-        HIPC(launch_noise_raw(ws.noise.f(), S, B, h->n_classes, (const RowInfo*)ws.rows.p,
-                              (uint32_t)(h->seed & 0xffffffffu), (uint32_t)(h->seed >> 32),
-                              h->stream));
-    HIPC(prepare_stage(h->stages[0].K, h->RT));
+        CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, B,
+                           plan[u].row0, plan[u].fbase));
+    HIPC(prepare_stage(h->stages[0].K, h->RT, h->nrg));
     {
         const char* env = std::getenv("WRNN_PHASE_STEP");
         h->phase_step = env ? std::atoi(env) : -1;
@@ -1030,7 +1030,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                             b.nseg = 1;
                             b.tile_start[0] = 0;
                             b.tile_start[1] = a.seg[k].n_tiles;
-                            HIPC(launch_stage(b, K, h->RT, h->nrt, h->stream));
+                            HIPC(launch_stage(b, K, h->RT, h->nrg, h->nrt, h->stream));
                         }
                 }
         }
@@ -1052,7 +1052,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         sa.rows = (const RowInfo*)ws.rows.p;
         HIPC(launch_sample(sa, h->stream));
     }
-    HIPC(prepare_stage(h->stages[0].K, h->RT));
+    HIPC(prepare_stage(h->stages[0].K, h->RT, h->nrg));
     if (h->timing) {
         const size_t need = ((size_t)S / kStampEvery + 1) * h->stages.size() * kMaxStampWG * 2 *
                             sizeof(uint32_t);
@@ -1375,10 +1375,16 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
 }
 
 int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity) {
+    // the sampler draws its noise in-kernel from philox.h; this regenerates the same stream
+    // for the last call's rows with the same device code into a scratch buffer
     if (!h || !out) return fail(WRNN_ERR_INVALID, "null argument");
     if (h->cfg.mode != WRNN_MODE_RAW) return fail(WRNN_ERR_INVALID, "RAW mode only");
     const size_t n = (size_t)n_steps * h->last_B * h->n_classes;
     if (n_steps > h->last_S || capacity < n) return fail(WRNN_ERR_CAPACITY, "capacity");
+    CHECK(h->ws.noise.alloc(n * sizeof(float)));
+    HIPC(launch_noise_raw(h->ws.noise.f(), n_steps, h->last_B, h->n_classes,
+                          (const RowInfo*)h->ws.rows.p, (uint32_t)(h->seed & 0xffffffffu),
+                          (uint32_t)(h->seed >> 32), h->stream));
     HIPC(hipStreamSynchronize(h->stream));
     HIPC(hipMemcpy(out, h->ws.noise.p, n * sizeof(float), hipMemcpyDeviceToHost));
     return WRNN_OK;

@@ -19,12 +19,16 @@ enum EpiKind : int {
     EPI_COND_RELU = 3,  // out[r][o] = relu(acc + cond(frame)[o])
 };
 
-// Tile shapes: OPL outputs per thread, NOG output groups per tile, KC = 256/NOG k-chunks.
+// Tile shapes (256 threads = NOG output groups x NRG row groups x KC k-chunks):
+//   TILE_GATE: OPL 3 = the r,z,n gates of one unit per thread, NOG 4 units per tile
+//   TILE_OUT : OPL 1 output per thread, NOG 4 outputs per tile
+// NRG (1, 2 or 4) is a launch-wide template parameter chosen by the runtime.
 enum TileCfg : int {
-    CFG3 = 0,  // OPL 3 (the r,z,n gates of one unit), 4 units per tile  (OT 12)
-    CFG2 = 1,  // OPL 2, 8 groups (OT 16)
-    CFG1 = 2,  // OPL 1, 4 groups (OT 4)
+    TILE_GATE = 0,
+    TILE_OUT = 1,
 };
+constexpr int kTileNOG = 4;
+inline int tile_opl(int cfg) { return cfg == TILE_GATE ? 3 : 1; }
 
 struct RowInfo {
     int pos0;        // global index of this row's step-0 position in per-position buffers
@@ -82,7 +86,7 @@ struct SampleArgs {
     const float* gh1;      // [r][3H] = W_hh1 h1 + b_hh1
     float* h1;             // [r][H] in/out
     float* x1;             // [r][H] out: xI + h1
-    const float* cI;       // per position [p][H]: I.weight[:,1:] . [m, a1[:31]] + I.bias
+    const float* cI;       // folded [t][r][H]: I.weight[:,1:] . [m, a1[:31]] + I.bias
     const float* w0;       // [H] = I.weight[:, 0]
     const RowInfo* rows;
     uint32_t k0, k1;       // Philox key (MOL draws in-kernel)
@@ -97,11 +101,13 @@ struct GemmA {  // A(m, k)
     int kind;   // 0: row-major W[m*ld + k]; 1: cond-A (mel/aux gather for cI); 2: frame-A
     const float* p;
     int ld;
-    // kind 1: mel_up channel-major [80][ldm] + R channel-major [C][T]
+    // kind 1: row m = (step t = m / Bu, fold f = m % Bu) -> position p = f * tpo + t;
+    // mel_up channel-major [n_mel][ldm] + R channel-major [C][T]
     const float* mel;
     int ldm, n_mel, L, hop;
     const float* R;
     int ldr, r_off, n_aux;
+    int Bu, tpo;
 };
 struct GemmB {  // B(k, n)
     int kind;   // 0: row-major [k*ld + n]; 1: im2col of the zero-padded mel (conv_in)
@@ -110,7 +116,9 @@ struct GemmB {  // B(k, n)
     int T, pad, ksz;  // kind 1
 };
 struct GemmEp {
-    int kind;   // 0: +bias[n]; 1: +bias[m]; 2: BN(m) [+relu] [+res]
+    int kind;   // 0: +bias[n]; 1: +bias[m]; 2: BN(m) [+relu] [+res];
+                // 3: +bias[n] into folded row (m / Bu) * Btot + row0 + m % Bu
+    int Bu, Btot, row0;
     float* D;
     int ld;
     const float* bias;
@@ -121,8 +129,9 @@ struct GemmEp {
 };
 
 // launch wrappers (kernels_*.hip); return hipError_t
-hipError_t launch_stage(const StageArgs& a, int K, int RT, int n_row_tiles, hipStream_t s);
-hipError_t prepare_stage(int K, int RT);  // set the dynamic-LDS attribute (before capture)
+hipError_t launch_stage(const StageArgs& a, int K, int RT, int NRG, int n_row_tiles,
+                        hipStream_t s);
+hipError_t prepare_stage(int K, int RT, int NRG);  // dynamic-LDS attribute (before capture)
 hipError_t launch_sample(const SampleArgs& a, hipStream_t s);
 hipError_t launch_noise_raw(float* q, int S, int nrows, int n_classes, const RowInfo* rows,
                             uint32_t k0, uint32_t k1, hipStream_t s);
