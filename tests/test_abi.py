@@ -1,0 +1,69 @@
+"""The C-ABI library (include/wavernn_mi355x.h) loads and exports every declared symbol; host
+argument checking works without a GPU. CPU only (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, 'include', 'wavernn_mi355x.h')).read()
+    return sorted(set(re.findall(r'\b(wrnn_[a-z_]+)\s*\(', src)) - {'wrnn_progress_fn'})
+
+
+def test_header_and_binding_agree():
+    from wavernn_amd import _abi
+    assert sorted(_abi.EXPORTED) == declared_symbols()
+
+
+def test_library_exports_every_declared_symbol():
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.wrnn_version().startswith(b'wavernn-mi355x')
+
+
+def test_fold_shape_matches_reference_arithmetic():
+    """fold_with_overlap (fatchord_version.py:316-327) restated in the oracle vs the ABI."""
+    import torch
+    from oracle.wavernn_oracle import OracleWaveRNN
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    for T, tgt, ovl in [(1000, 11000, 550), (200, 11000, 550), (24, 1000, 100), (53, 3000, 1500),
+                        (71, 6000, 1000), (1, 100, 10), (7, 50, 0), (300, 8000, 800)]:
+        L = T * 200
+        b, s = ctypes.c_int(), ctypes.c_int()
+        assert lib.wrnn_fold_shape(T, 200, 1, tgt, ovl, ctypes.byref(b), ctypes.byref(s)) == 0
+        folded = OracleWaveRNN.fold_with_overlap(OracleWaveRNN, torch.zeros(1, L, 1), tgt, ovl)
+        assert (b.value, s.value) == tuple(folded.shape[:2]), (T, tgt, ovl)
+    assert lib.wrnn_fold_shape(10, 200, 0, 0, 0, ctypes.byref(b), ctypes.byref(s)) == 0
+    assert (b.value, s.value) == (1, 2000)
+
+
+def test_invalid_arguments_are_reported_not_crashed():
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    b, s = ctypes.c_int(), ctypes.c_int()
+    assert lib.wrnn_fold_shape(0, 200, 1, 100, 10, ctypes.byref(b), ctypes.byref(s)) == _abi.WRNN_ERR_INVALID
+    assert b'bad length' in lib.wrnn_last_error()
+    cfg = _abi.WrnnConfig()
+    cfg.model_type = 7
+    h = ctypes.c_void_p()
+    assert lib.wrnn_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == _abi.WRNN_ERR_INVALID
+    cfg.model_type, cfg.mode, cfg.bits = 0, 0, 9
+    cfg.n_upsample, cfg.hop_length = 3, 200
+    for i, f in enumerate((5, 5, 7)):
+        cfg.upsample_factors[i] = f
+    cfg.res_out_dims = 128
+    assert lib.wrnn_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == _abi.WRNN_ERR_INVALID
+    assert b'hop_length' in lib.wrnn_last_error()
+
+
+def test_product_fails_loudly_without_library(tmp_path):
+    from wavernn_amd import _abi
+    with pytest.raises(_abi.NativeLibraryMissing):
+        _abi.load_library(str(tmp_path / 'missing.so'))
