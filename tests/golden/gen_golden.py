@@ -65,8 +65,16 @@ def install_shims():
     for name in ('librosa', 'soundfile', 'WaveRNNVocoder'):
         if name not in sys.modules:
             sys.modules[name] = types.ModuleType(name)
-    if REF not in sys.path:
-        sys.path.insert(0, REF)
+    # the reference's `vocoder` (a namespace package: no __init__.py) must not be shadowed by
+    # this repo's drop-in `vocoder` shim (a regular package), so drop the shim's directory
+    # (wavernn_amd.synth is already imported)
+    sys.path[:] = [p for p in sys.path if not p.endswith('real-time-voice-cloning_amd')]
+    if REF in sys.path:
+        sys.path.remove(REF)
+    sys.path.insert(0, REF)
+    for mod in [m for m in sys.modules if m == 'vocoder' or m.startswith('vocoder.')]:
+        if 'real-time-voice-cloning_amd' in (getattr(sys.modules[mod], '__file__', '') or ''):
+            del sys.modules[mod]
 
 
 class NoiseState:
