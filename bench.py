@@ -42,7 +42,9 @@ def parse():
     ap.add_argument('--overlap', type=int, default=550)
     ap.add_argument('--cpu-seconds', type=float, default=15.0,
                     help='CPU-baseline sample budget (0 disables)')
-    ap.add_argument('--no-timing', action='store_true', help='disable in-kernel stage stamps')
+    ap.add_argument('--no-timing', action='store_true', help='disable kernel timing')
+    ap.add_argument('--engine', default='auto', choices=['auto', 'chain', 'persist'],
+                    help='recurrence engine (include/wavernn_mi355x.h WRNN_ENGINE_*)')
     return ap.parse_args()
 
 
@@ -93,6 +95,7 @@ def main():
                     mode=hp.mode, model_type=args.model, device=local)
     model.load_state_dict(sd)
     model.set_seed(1234)
+    model.set_engine(args.engine)
     U = args.utts_per_gpu
     mels_host = [synth_mel(args.frames, seed=rank * U + u) for u in range(U)]
     mels_dev = [torch.from_numpy(m / sp.max_abs_value).to(dev) for m in mels_host]
@@ -130,13 +133,17 @@ def main():
         dom = max(info, key=lambda r: (r[3] if r[3] == r[3] else 0) * r[4])
         name, by, fl, us, n = dom
         achieved = by / (us * 1e-6) / 1e9 if us > 0 else None
-        roof = {'bound': 'hbm', 'kernel': f'k_stage<{name}>', 'achieved': achieved,
+        kernel = 'k_persist' if name == 'persist' else f'k_stage<{name}>'
+        roof = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': None,
                 'avg_us': us, 'launches_timed': n, 'alg_bytes_per_launch': by,
                 'flops_per_launch': fl,
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
+        if name == 'persist':  # no progress callback -> one launch runs all S steps
+            S = model.fold_shape(args.frames, True, args.target, args.overlap)[1]
+            roof['us_per_step'] = us / S
     result = {
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',
         'value': value, 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -151,7 +158,8 @@ def main():
                    'utts_per_gpu': U, 'frames': args.frames,
                    'fold_rows_per_gpu': U * model.fold_shape(args.frames, True, args.target,
                                                              args.overlap)[0],
-                   'parallelism': f'utterances sharded over {world} GPU(s), no collective'},
+                   'parallelism': f'utterances sharded over {world} GPU(s), no collective',
+                   'engine': model.last_engine()},
         'roofline': roof,
         'cpu_baseline': None,
     }

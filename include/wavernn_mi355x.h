@@ -54,6 +54,15 @@ extern "C" {
 #define WRNN_MODE_RAW 0 /* softmax over 2**bits classes, Categorical sample */
 #define WRNN_MODE_MOL 1 /* 10-component discretized mixture of logistics   */
 
+/* Recurrence engines (same results, different schedules):
+ *   CHAIN   one launch per layer group per step, HIP-graph captured (every topology)
+ *   PERSIST one persistent weight-stationary launch per chunk of steps, 8 XCD-local groups
+ *           (fatchord, rnn_dims = fc_dims = 512, <= 32 fold rows, n_classes <= 1024)
+ *   AUTO    PERSIST when the call qualifies, else CHAIN (default; env WRNN_ENGINE overrides) */
+#define WRNN_ENGINE_AUTO 0
+#define WRNN_ENGINE_CHAIN 1
+#define WRNN_ENGINE_PERSIST 2
+
 /* Topology, with the field names of config/hparams.py:220-285 / :356-421. */
 typedef struct wrnn_config {
     int model_type;         /* WRNN_MODEL_*                         */
@@ -125,9 +134,16 @@ int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* m
                                int16_t* labels_dev, float* samples_dev, size_t capacity,
                                int* row_offset, int* seq_len, wrnn_progress_fn cb, void* user);
 
-/* Per-stage timing of the dominant recurrent kernel (in-kernel s_memrealtime stamps,
- * 100 MHz). Enable before a call; read after: average duration in microseconds of the
- * launches of stage `stage` in the last call, and the number of launches averaged. */
+/* Select the recurrence engine for later calls (WRNN_ENGINE_*). Requesting PERSIST for a
+ * call that does not qualify makes that call fail with WRNN_ERR_INVALID. */
+int wrnn_set_engine(wrnn_handle* h, int engine);
+/* Engine that ran the last call. */
+int wrnn_last_engine(wrnn_handle* h, int* engine);
+
+/* Per-stage timing of the dominant recurrent kernel. Enable before a call; read after:
+ * average duration in microseconds of the launches of stage `stage` in the last call, and
+ * the number of launches averaged. CHAIN: in-kernel s_memrealtime stamps (100 MHz) of every
+ * 8th step. PERSIST: one stage, HIP events recorded on the launch stream around each launch. */
 int wrnn_enable_stage_timing(wrnn_handle* h, int enable);
 int wrnn_stage_timing(wrnn_handle* h, int stage, double* avg_us, int* launches);
 /* Name and algorithmic bytes / FLOPs per launch of stage `stage` for the last call's shape. */

@@ -1,0 +1,724 @@
+// Persistent, weight-stationary recurrence of the fatchord WaveRNN (the "persist" engine).
+//
+// Reference step body: vocoder/models/fatchord_version.py:192-236. One launch runs a chunk of
+// steps for all fold rows. The 256 workgroups (one per CU, 512 threads) form 8 groups from the
+// workgroups that report the same HW_REG_XCC_ID, so every group lives on one XCD and shares
+// its L2. Group g owns fold rows g, g+8, ... (NR rows; the host pads the row count to 8*NR)
+// and holds ALL step weights, spread over its 32 workgroups (slot w owns GRU units / outputs
+// [16w, 16w+16) and fc3 classes [cpw*w, cpw*(w+1))): registers hold W_ih2[:, :512] and W_hh1
+// (r,z,n rows of the slot's units) and the fc1/fc2 rows; LDS holds the W_hh2 rows and the fc3
+// rows (registers when a slot owns more than 16 classes, i.e. 10-bit). Nothing is re-read from
+// HBM per step except the precomputed per-step inputs (P1, cI, per-frame aux terms, Gumbel
+// noise), all issued at the top of the step so their latency hides behind the exchanges.
+//
+// Per step, four in-group exchanges (plain stores -> s_waitcnt vmcnt(0) -> workgroup barrier ->
+// one plain flag store per workgroup; consumers poll the 32 flags and read the payload with
+// non-temporal loads, which are served by the XCD's shared L2; measured stale-free and ~1.3 us
+// per hop on MI355X, tools/microbench_xcd.hip):
+//   A: GRU2 (W_ih2 x1 + cond, gh2 of the previous step) -> x2, h2 ; W_hh1 h1 + b -> gh1
+//   B: fc1 (relu) on x2                   ; W_hh2 h2 + b -> gh2 for the next step (kept local)
+//   C: fc2 (relu) on y1
+//   D: fc3 on y2 -> per-slot Gumbel-max candidates (RAW) or logits (MOL)
+// and, redundantly in every workgroup: the sample of step t and GRU1 of step t+1 for all 512
+// units (so x1/h1 never need an exchange).
+// Sampling: argmax_k (l_k + g_k), g_k = -log q_k with q the RNG contract's Exp(1) variate --
+// the same decision as the reference's argmax((softmax(l)/sum)/q) in exact arithmetic.
+// Every spin is bounded; on a timeout the kernel sets an error code and every group exits.
+#include "wrnn_kernels.h"
+#include "philox.h"
+
+namespace wrnn {
+
+constexpr unsigned kSpinTicks = 100000000u;  // 1 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ unsigned p_now() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned ld_nt_u(const unsigned* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float ld_nt_f(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float4 ld_nt_f4(const float4* p) {
+    const float* q = reinterpret_cast<const float*>(p);
+    return make_float4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
+                       __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
+}
+__device__ __forceinline__ unsigned ld_sc1_u(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float pdpp(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 16 lanes of a DPP row; every lane of the row receives the same total
+__device__ __forceinline__ float row16_sum(float v) {
+    v += pdpp<0xB1>(v);   // quad_perm xor 1
+    v += pdpp<0x4E>(v);   // quad_perm xor 2
+    v += pdpp<0x124>(v);  // row_ror 4
+    v += pdpp<0x128>(v);  // row_ror 8
+    return v;
+}
+
+__device__ __forceinline__ float p_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+// torch GRUCell gate arithmetic (same operation order as kernels_step.hip gru_cell)
+__device__ __forceinline__ float p_gru(float gi_r, float gi_z, float gi_n, float gh_r, float gh_z,
+                                       float gh_n, float h) {
+#pragma clang fp contract(off)
+    const float r = p_sigmoid(gh_r + gi_r);
+    const float z = p_sigmoid(gh_z + gi_z);
+    const float ghr = gh_n * r;
+    const float n = tanhf(gi_n + ghr);
+    const float d = h - n;
+    const float dz = d * z;
+    return dz + n;
+}
+__device__ __forceinline__ float p_add(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+
+// packed fp32 (v_pk_fma_f32): even/odd-k partial sums of one (output, row) dot product
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void dot4(v2f& acc, const float4 w, const float4 x) {
+    acc = __builtin_elementwise_fma((v2f){w.x, w.y}, (v2f){x.x, x.y}, acc);
+    acc = __builtin_elementwise_fma((v2f){w.z, w.w}, (v2f){x.z, x.w}, acc);
+}
+__device__ __forceinline__ float hsum(const v2f a) { return a.x + a.y; }
+
+__device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
+    const int rel = ri.rel0 + t;
+    return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
+}
+
+// exchange area per group (floats): A double-buffered [r][x2 | h2 | gh1(3H)], B y1, C y2, D
+constexpr int XB_A = 0;
+constexpr int XB_A_SZ = kPNR * 5 * kPH;
+constexpr int XB_B = XB_A + 2 * XB_A_SZ;
+constexpr int XB_C = XB_B + kPNR * kPH;
+constexpr int XB_D = XB_C + kPNR * kPH;
+constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][value, class]
+constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
+constexpr int XB_GROUP = XB_D + XB_D_SZ + 64;
+
+// LDS carve (floats). The per-step operands come first so every ds_read offset of the inner
+// loops fits the 16-bit immediate (no per-(q, row) address registers).
+constexpr int L_X0 = 0;                             // [kPNR][512]
+constexpr int L_X1 = L_X0 + kPNR * kPH;             // [kPNR][512]
+constexpr int L_RED = L_X1 + kPNR * kPH;            // [32 og][kPNR][2]
+constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
+constexpr int L_W = L_SX + 16;                      // slot weights (kPLdsW4 float4)
+constexpr int L_FC3 = L_W + 16 * 3 * kPH;           // fc3 rows inside the weight block
+constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
+
+__device__ __forceinline__ bool p_wait(const unsigned* f, unsigned target, unsigned* ctl, int tid) {
+    // wave 0 polls the group's 32 flags; every wave then meets at the barrier
+    __shared__ int s_fail;
+    if (tid < 64) {
+        const unsigned t0 = p_now();
+        unsigned n = 0;
+        bool ok = true;
+        while (true) {
+            const unsigned v = tid < kPM ? ld_nt_u(f + tid) : target;
+            if (__all(v >= target)) break;
+            if ((++n & 255) == 0) {
+                if (ld_sc1_u(ctl + PC_ERR)) {
+                    ok = false;
+                    break;
+                }
+                if (p_now() - t0 > kSpinTicks) {
+                    if (tid == 0) atomicMax(ctl + PC_ERR, 2u);
+                    ok = false;
+                    break;
+                }
+            }
+        }
+        if (tid == 0) s_fail = ok ? 0 : 1;
+    }
+    __syncthreads();
+    return s_fail == 0;
+}
+
+__device__ __forceinline__ void p_publish(unsigned* flag, unsigned value, int tid) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// argmax over the 32 lanes of a half-wave (value, class); ties -> lowest class
+__device__ __forceinline__ void half_argmax(float& v, int& k) {
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) {
+        const float v2 = __shfl_xor(v, m, 32);
+        const int k2 = __shfl_xor(k, m, 32);
+        if (v2 > v || (v2 == v && k2 < k)) {
+            v = v2;
+            k = k2;
+        }
+    }
+}
+
+// Buffer-resource access: a uniform (SGPR) base and a 32-bit per-lane byte offset, so no
+// 64-bit per-lane addresses stay live across the step loop.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kCpNT = 2;  // cache policy: non-temporal (served by L2, bypasses the CU's L1)
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float bld(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ float bld_nt(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kCpNT));
+}
+__device__ __forceinline__ float4 bld4_nt(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kCpNT));
+}
+__device__ __forceinline__ void bst(float v, rsrc_t r, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+
+template <int NR, bool FC3R>
+__global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    const int tid = threadIdx.x;
+    // ---- group formation (placement-independent: a group is whatever shares an XCD) ----
+    if (tid == 0) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        const int g = x & 7;
+        s_group = g;
+        s_slot = (int)atomicAdd(a.ctl + PC_REG + g, 1u);
+        atomicAdd(a.ctl + PC_TOTAL, 1u);
+        const unsigned t0 = p_now();
+        int ok = 1;
+        while (ld_sc1_u(a.ctl + PC_TOTAL) < (unsigned)(kPG * kPM)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (p_now() - t0 > kSpinTicks) {
+                ok = 0;
+                atomicMax(a.ctl + PC_ERR, 1u);
+                break;
+            }
+        }
+        if (ok)
+            for (int i = 0; i < kPG; ++i)
+                if (ld_sc1_u(a.ctl + PC_REG + i) != (unsigned)kPM) {
+                    ok = 0;
+                    atomicMax(a.ctl + PC_ERR, 3u);
+                }
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    const int og = tid >> 4, kc = tid & 15;
+    constexpr int H = kPH;
+    const int u = 16 * w + (og & 15);   // unit / output of this thread's weight rows
+    const bool gate_a = og < 16;        // stage A: W_ih2 (og<16) | W_hh1 (og>=16)
+    const int cls = a.cpw * w + og;     // fc3 class of this thread
+    const bool has_cls = og < a.cpw && cls < a.n_classes;
+    unsigned* fl = a.flags + (size_t)g * 4 * 64;
+    const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * XB_GROUP);  // this group's exchange area
+    const bool trace = a.phases != nullptr;
+    uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
+#define PSTAMP(i) \
+    if (trace && t == a.phase_t && tid == 0) ph[i] = p_now()
+
+    // ---- weights: registers and LDS -----------------------------------------------------
+    constexpr int NW = FC3R ? 40 : 32;
+    float4 wr[NW];
+    {
+        const float4* src = a.wreg + ((size_t)w * kPT + tid) * NW;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) wr[i] = src[i];
+        const float4* hs = a.wlds + (size_t)w * kPLdsW4;
+        float4* hd = reinterpret_cast<float4*>(lds + L_W);
+        const int n4 = FC3R ? 16 * 3 * kPK4 : kPLdsW4;
+        for (int i = tid; i < n4; i += kPT) hd[i] = hs[i];
+    }
+    // ---- chunk state -----------------------------------------------------------------------
+    // thread tid = unit j of the redundant GRU1; lanes kc < NR of og < 16 own (u, row kc) of GRU2
+    float h1[NR], h2r = 0.f, gh2r[3] = {0.f, 0.f, 0.f};
+    const bool own = gate_a && kc < NR;
+    const int lr = kc < NR ? kc : 0;
+    const int lrow = g + kPG * lr;  // row of this lane's epilogue
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int row = g + kPG * r;
+        h1[r] = a.st_h1[(size_t)row * H + tid];
+        lds[L_X0 + r * kPH + tid] = a.st_x1[(size_t)row * H + tid];
+        lds[L_X1 + r * kPH + tid] = h1[r];
+    }
+    if (own) {
+        h2r = a.st_h2[(size_t)lrow * H + u];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gh2r[j] = a.st_gh2[(size_t)lrow * 3 * H + j * H + u];
+    }
+    // per-thread constants
+    const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid], w0j = a.w0[tid];
+    float b3[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) b3[j] = gate_a ? a.b_hh2[j * H + u] : a.b_hh1[j * H + u];
+    const float bcls = has_cls ? a.b_fc3[cls] : 0.f;
+    const RowInfo lri = a.rows[lrow];
+    // per-lane byte offsets (32-bit)
+    const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
+    const unsigned o_P1 = (unsigned)(g * 3 * H + tid) * 4u;             // P1 row g, unit tid
+    const unsigned o_cI = (unsigned)(g * H + tid) * 4u;                 // cI row g, unit tid
+    const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 4u;             // bufA row lr, unit u
+    const unsigned o_y = (unsigned)(lr * kPH + u) * 4u;                 // bufB/C row lr, unit u
+    const unsigned o_gum = (unsigned)(lrow * a.n_classes + cls) * 4u;   // gumbel row lrow
+    const rsrc_t fcr = mk_rsrc(a.fcond);
+    const unsigned o_fc = (unsigned)((gate_a ? a.oG2 : a.oF1) + u) * 4u;
+    const unsigned o_f2 = (unsigned)(a.oF2 + u) * 4u;
+    __syncthreads();
+
+    const float4* X0 = reinterpret_cast<const float4*>(lds + L_X0);
+    const float4* X1 = reinterpret_cast<const float4*>(lds + L_X1);
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
+    for (int t = a.t0; t < a.t1; ++t) {
+        const unsigned seq = (unsigned)t + 1u;
+        const unsigned sA = (unsigned)(XB_A + (t & 1) * XB_A_SZ) * 4u;  // bufA of this step
+        PSTAMP(0);
+        // ---- per-step inputs, issued now, consumed at the epilogues / GRU1 ------------------
+        float pP[NR][3], pC[NR];
+        const bool nxt = t + 1 < a.S;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) pP[r][0] = pP[r][1] = pP[r][2] = pC[r] = 0.f;
+        if (nxt) {
+            const rsrc_t pr = mk_rsrc(a.P1 + (size_t)(t + 1) * a.B * 3 * H);
+            const rsrc_t cr = mk_rsrc(a.cI + (size_t)(t + 1) * a.B * H);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    pP[r][j] = bld(pr, o_P1, (unsigned)(r * kPG * 3 * H + j * H) * 4u);
+                pC[r] = bld(cr, o_cI, (unsigned)(r * kPG * H) * 4u);
+            }
+        }
+        float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f;
+        if (kc < NR) {
+            const unsigned fo = (unsigned)(p_frame(lri, t, a.hop) * a.cond_width) * 4u;
+            pc0 = bld(fcr, o_fc + fo, 0);
+            if (gate_a) {
+                pc1 = bld(fcr, o_fc + fo, H * 4);
+                pc2 = bld(fcr, o_fc + fo, 2 * H * 4);
+                pf2 = bld(fcr, o_f2 + fo, 0);
+            }
+            if (has_cls && a.mode == 0)
+                pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes), o_gum, 0);
+        }
+        // ================= stage A: GRU2 (og<16) | W_hh1 h1 (og>=16) =================
+        {
+            v2f acc[3][NR];
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc[j][r] = (v2f){0.f, 0.f};
+            const float4* Xs = gate_a ? X0 : X1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const float4 x4 = Xs[r * kPK4 + 16 * q + kc];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) dot4(acc[j][r], wr[j * 8 + q], x4);
+                }
+            }
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[0][r]));
+                const float t1 = row16_sum(hsum(acc[1][r]));
+                const float t2 = row16_sum(hsum(acc[2][r]));
+                if (kc == r) {
+                    s0 = t0;
+                    s1 = t1;
+                    s2 = t2;
+                }
+            }
+            if (kc < NR) {
+                if (gate_a) {
+                    const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2),
+                                           gh2r[0], gh2r[1], gh2r[2], h2r);
+                    h2r = hn;
+                    bst(p_add(lds[L_X0 + lr * kPH + u], hn), xr, o_u, sA);  // x2 = x1 + h2
+                    bst(hn, xr, o_u, sA + kPH * 4);
+                } else {
+                    bst(p_add(s0, b3[0]), xr, o_u, sA + 2 * kPH * 4);
+                    bst(p_add(s1, b3[1]), xr, o_u, sA + 3 * kPH * 4);
+                    bst(p_add(s2, b3[2]), xr, o_u, sA + 4 * kPH * 4);
+                }
+            }
+        }
+        PSTAMP(1);
+        p_publish(fl + 0 * 64 + w, seq, tid);
+        if (!p_wait(fl + 0 * 64, seq, a.ctl, tid)) return;
+        PSTAMP(2);
+        // ================= stage B: fc1 (og>=16) | W_hh2 h2 (og<16, LDS weights) ======
+        for (int i = tid; i < NR * kPK4; i += kPT) {
+            const int r = i / kPK4, q = i % kPK4;
+            const unsigned o = (unsigned)(r * 5 * kPH + 4 * q) * 4u;
+            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, o, sA);
+            reinterpret_cast<float4*>(lds + L_X1)[i] = bld4_nt(xr, o, sA + kPH * 4);
+        }
+        __syncthreads();
+        if (gate_a) {
+            v2f acc[3][NR];
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc[j][r] = (v2f){0.f, 0.f};
+            const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)og * 3 * kPK4;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                float4 w4[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) dot4(acc[j][r], w4[j], x4);
+                }
+            }
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[0][r]));
+                const float t1 = row16_sum(hsum(acc[1][r]));
+                const float t2 = row16_sum(hsum(acc[2][r]));
+                if (kc == r) {
+                    s0 = t0;
+                    s1 = t1;
+                    s2 = t2;
+                }
+            }
+            if (kc < NR) {  // gh2 for the next step stays in this lane
+                gh2r[0] = p_add(s0, b3[0]);
+                gh2r[1] = p_add(s1, b3[1]);
+                gh2r[2] = p_add(s2, b3[2]);
+            }
+        } else {
+            v2f acc[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) dot4(acc[r], wr[24 + q], X0[r * kPK4 + 16 * q + kc]);
+            }
+            float s0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[r]));
+                if (kc == r) s0 = t0;
+            }
+            if (kc < NR) {
+                const float y = p_add(s0, pc0);
+                bst(y > 0.f ? y : 0.f, xr, o_y, XB_B * 4);
+            }
+        }
+        PSTAMP(3);
+        p_publish(fl + 1 * 64 + w, seq, tid);
+        if (!p_wait(fl + 1 * 64, seq, a.ctl, tid)) return;
+        PSTAMP(4);
+        // ================= stage C: fc2 (og<16) ============================================
+        for (int i = tid; i < NR * kPK4; i += kPT)
+            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_B * 4);
+        __syncthreads();
+        if (gate_a) {
+            v2f acc[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) dot4(acc[r], wr[24 + q], X0[r * kPK4 + 16 * q + kc]);
+            }
+            float s0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[r]));
+                if (kc == r) s0 = t0;
+            }
+            if (kc < NR) {
+                const float y = p_add(s0, pf2);
+                bst(y > 0.f ? y : 0.f, xr, o_y, XB_C * 4);
+            }
+        }
+        PSTAMP(5);
+        p_publish(fl + 2 * 64 + w, seq, tid);
+        if (!p_wait(fl + 2 * 64, seq, a.ctl, tid)) return;
+        PSTAMP(6);
+        // ================= stage D: fc3 -> candidates =======================================
+        float pG[NR][3];  // gh1 of GRU1(t+1) (published at hop A)
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                pG[r][j] = bld_nt(xr, o_tid, sA + (unsigned)(r * 5 * kPH + (2 + j) * kPH) * 4u);
+        for (int i = tid; i < NR * kPK4; i += kPT)
+            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_C * 4);
+        __syncthreads();
+        {
+            v2f acc[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+            if (has_cls) {
+                const float4* Wf = reinterpret_cast<const float4*>(lds + L_FC3) + (size_t)og * kPK4;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float4 w4 = FC3R ? wr[(32 + q) % NW] : Wf[16 * q + kc];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) dot4(acc[r], w4, X0[r * kPK4 + 16 * q + kc]);
+                }
+            }
+            float s0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[r]));
+                if (kc == r) s0 = t0;
+            }
+            float* red = lds + L_RED;  // [og][r][value, class]
+            if (kc < NR) {
+                float val = -INFINITY;
+                if (has_cls) {
+                    const float l = p_add(s0, bcls);
+                    if (a.mode == 0)
+                        val = p_add(l, pgum);
+                    else  // MOL: logits row
+                        bst(l, xr, (unsigned)(kc * 64 + cls) * 4u, (XB_D + XB_D_LOG) * 4);
+                }
+                red[(og * kPNR + kc) * 2] = val;
+                red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
+            }
+            __syncthreads();
+            if (a.mode == 0 && tid < NR) {
+                const int r = tid;
+                float bv = -INFINITY;
+                int bi = 0x7fffffff;
+                for (int o = 0; o < a.cpw; ++o) {
+                    const float v2 = red[(o * kPNR + r) * 2];
+                    const int i2 = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                    if (v2 > bv || (v2 == bv && i2 < bi)) {
+                        bv = v2;
+                        bi = i2;
+                    }
+                }
+                const unsigned o = (unsigned)((w * kPNR + r) * 2) * 4u;
+                bst(bv, xr, o, XB_D * 4);
+                bst(__int_as_float(bi), xr, o + 4, XB_D * 4);
+            }
+        }
+        PSTAMP(7);
+        p_publish(fl + 3 * 64 + w, seq, tid);
+        if (!p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
+        PSTAMP(8);
+        // ================= sample of step t (redundant in every workgroup) ==================
+        if (a.mode == 0) {
+            if (tid < 32 * NR) {  // half-wave r: lane o holds slot o's candidate
+                const int r = tid >> 5, o = tid & 31;
+                const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
+                float bv = bld_nt(xr, off, XB_D * 4);
+                int bi = __float_as_int(bld_nt(xr, off + 4, XB_D * 4));
+                half_argmax(bv, bi);
+                if (o == 0) {
+                    float xv;
+                    {
+#pragma clang fp contract(off)
+                        xv = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
+                    }
+                    lds[L_SX + r] = xv;
+                    if (w == 0) {
+                        const int row = g + kPG * r;
+                        a.labels[(size_t)row * a.ld + t] = (int16_t)bi;
+                        a.samples[(size_t)row * a.ld + t] = xv;
+                    }
+                }
+            }
+        } else if (tid < NR) {
+            // MOL: vocoder/distribution.py:104-140 with the Philox draws (kernels_step.hip)
+            const int r = tid, row = g + kPG * r;
+            const RowInfo ri = a.rows[row];
+            const unsigned lo = (unsigned)(r * 64) * 4u;
+            const unsigned so = (XB_D + XB_D_LOG) * 4;
+            uint32_t wd[11];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const U4 o4 = philox4x32_10(kMolDomain | (uint32_t)j, (uint32_t)t, (uint32_t)ri.fold,
+                                            ri.stream, a.k0, a.k1);
+                wd[4 * j] = o4.x;
+                wd[4 * j + 1] = o4.y;
+                wd[4 * j + 2] = o4.z;
+                if (j < 2) wd[4 * j + 3] = o4.w;
+            }
+            float xv;
+            {
+#pragma clang fp contract(off)
+                float bv = -INFINITY;
+                int bi = 0;
+                for (int k = 0; k < 10; ++k) {
+                    const float u1 = mol_uniform_from_u32(wd[k]);
+                    const float v2 = bld_nt(xr, lo + 4u * k, so) - logf(-logf(u1));
+                    if (v2 > bv) {
+                        bv = v2;
+                        bi = k;
+                    }
+                }
+                const float u2 = mol_uniform_from_u32(wd[10]);
+                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
+                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
+                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                ls = ls < lsmin ? lsmin : ls;
+                const float lu = logf(u2) - logf(1.0f - u2);
+                xv = mean + expf(ls) * lu;
+                xv = xv < -1.f ? -1.f : xv;
+                xv = xv > 1.f ? 1.f : xv;
+            }
+            lds[L_SX + r] = xv;
+            if (w == 0) a.samples[(size_t)row * a.ld + t] = xv;
+        }
+        __syncthreads();
+        PSTAMP(9);
+        if (!nxt) continue;
+        // ================= GRU1 of step t+1 for all 512 units (redundant) ===================
+        //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const float x = lds[L_SX + r];
+            const float hn = p_gru(fmaf(vj0, x, pP[r][0]), fmaf(vj1, x, pP[r][1]),
+                                   fmaf(vj2, x, pP[r][2]), pG[r][0], pG[r][1], pG[r][2], h1[r]);
+            h1[r] = hn;
+            lds[L_X0 + r * kPH + tid] = p_add(fmaf(w0j, x, pC[r]), hn);
+            lds[L_X1 + r * kPH + tid] = hn;
+        }
+        __syncthreads();
+        PSTAMP(10);
+    }
+#undef PSTAMP
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+    // ---- save the chunk state --------------------------------------------------------------
+    if (a.t1 < a.S) {
+        if (w == 0)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int row = g + kPG * r;
+                a.st_x1[(size_t)row * H + tid] = lds[L_X0 + r * kPH + tid];
+                a.st_h1[(size_t)row * H + tid] = lds[L_X1 + r * kPH + tid];
+            }
+        if (own) {
+            a.st_h2[(size_t)lrow * H + u] = h2r;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a.st_gh2[(size_t)lrow * 3 * H + j * H + u] = gh2r[j];
+        }
+    }
+}
+
+// Step-0 state: GRU1 with x = 0, h = 0, gh = b_hh1 -> x1(0), h1(0); h2 = 0, gh2 = b_hh2.
+__global__ __launch_bounds__(kPT) void k_persist_init(PersistArgs a) {
+    const int row = blockIdx.x, j = threadIdx.x, H = kPH;
+    const float* P1 = a.P1 + (size_t)row * 3 * H;  // step 0
+    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
+                           a.b_hh1[2 * H + j], 0.f);
+    a.st_h1[(size_t)row * H + j] = hn;
+    a.st_x1[(size_t)row * H + j] = p_add(a.cI[(size_t)row * H + j], hn);
+    a.st_h2[(size_t)row * H + j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.st_gh2[(size_t)row * 3 * H + k * H + j] = a.b_hh2[k * H + j];
+}
+
+hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_persist_init, dim3(a.B), dim3(kPT), 0, s, a);
+    return hipGetLastError();
+}
+
+// RAW Gumbel noise g = -log(q), q the contract's Exp(1) variate (philox.h exp1_from_u32):
+// argmax_k (l_k + g_k) is the decision of argmax_k ((softmax(l)_k / sum) / q_k).
+__global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int ng,
+                                                const RowInfo* rows, uint32_t k0, uint32_t k1) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r, k4)
+    const size_t total = (size_t)S * nrows * ng;
+    if (i >= total) return;
+    const int k4 = (int)(i % ng);
+    const size_t tr = i / ng;
+    const int r = (int)(tr % nrows), t = (int)(tr / nrows);
+    const RowInfo ri = rows[r];
+    const U4 o = philox4x32_10((uint32_t)k4, (uint32_t)t, (uint32_t)ri.fold, ri.stream, k0, k1);
+    float4 v;
+    v.x = (float)(-log((double)exp1_from_u32(o.x)));
+    v.y = (float)(-log((double)exp1_from_u32(o.y)));
+    v.z = (float)(-log((double)exp1_from_u32(o.z)));
+    v.w = (float)(-log((double)exp1_from_u32(o.w)));
+    g[i] = v;
+}
+
+hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
+                         uint32_t k0, uint32_t k1, hipStream_t s) {
+    if (n_classes % 4) return hipErrorInvalidValue;
+    const int ng = n_classes / 4;
+    const size_t total = (size_t)S * nrows * ng;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gumbel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<float4*>(g), S, nrows, ng, rows, k0, k1);
+    return hipGetLastError();
+}
+
+size_t persist_flag_words() { return (size_t)kPG * 4 * 64; }
+size_t persist_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
+size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
+
+template <int NR, bool FC3R>
+hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
+    static bool attr = false;
+    const size_t lds = persist_lds_bytes();
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_persist<NR, FC3R>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NR, bool FC3R>
+int persist_spill_t() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+// 1 when the (rows per group, classes per slot) variant exists and keeps its state in
+// registers (no scratch spills: scratch traffic would serialise behind every exchange).
+int persist_variant_ok(int nr, int cpw) {
+    if (cpw < 1 || cpw > kPCls) return 0;
+    const bool r = cpw > 16;
+    int sp = -1;
+    switch (nr) {
+        case 1: sp = r ? persist_spill_t<1, true>() : persist_spill_t<1, false>(); break;
+        case 2: sp = r ? persist_spill_t<2, true>() : persist_spill_t<2, false>(); break;
+        case 3: sp = r ? persist_spill_t<3, true>() : persist_spill_t<3, false>(); break;
+        case 4: sp = r ? persist_spill_t<4, true>() : persist_spill_t<4, false>(); break;
+        default: break;
+    }
+    return sp == 0 ? 1 : 0;
+}
+
+hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
+    if (a.B != kPG * a.nr || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)
+        return hipErrorInvalidValue;
+    const bool r = a.cpw > 16;
+    switch (a.nr) {
+        case 1: return r ? launch_persist_t<1, true>(a, s) : launch_persist_t<1, false>(a, s);
+        case 2: return r ? launch_persist_t<2, true>(a, s) : launch_persist_t<2, false>(a, s);
+        case 3: return r ? launch_persist_t<3, true>(a, s) : launch_persist_t<3, false>(a, s);
+        case 4: return r ? launch_persist_t<4, true>(a, s) : launch_persist_t<4, false>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace wrnn

@@ -168,7 +168,27 @@ struct wrnn_handle {
     int nrg = 2;  // row groups per stage tile (env WRNN_NRG: 1, 2 or 4)
     std::vector<RowInfo> rows_host;
 
+    // ---- persistent engine (kernels_persist.hip)
+    struct PersistW {
+        bool ok = false;  // weights packed: fatchord, rnn_dims = fc_dims = 512, n <= 1024
+        int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;
+        const float *wreg = nullptr, *wlds = nullptr, *WIh1T = nullptr;
+        const float *b_ih1 = nullptr, *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;
+    } pw;
+    struct PersistWS {
+        DevBuf P1, gumbel, ctl, flags, xbuf, st, stamps, phases;
+    } pws;
+    int engine = WRNN_ENGINE_AUTO;  // requested engine (wrnn_set_engine / env WRNN_ENGINE)
+    int last_engine = WRNN_ENGINE_CHAIN;
+    bool persist_failed = false;    // a persistent launch failed on this device: stay on CHAIN
+    int last_Bp = 0;                // rows the last call ran (padded to 8 * rows-per-group)
+    std::vector<hipEvent_t> pev;    // PERSIST timing events (start, end) per launch
+    std::vector<int> pev_steps;
+    double p_step_bytes = 0, p_step_flops = 0;  // algorithmic per step
+    double p_avg_steps = 0;                      // steps per timed launch
+
     ~wrnn_handle() {
+        for (auto e : pev) (void)hipEventDestroy(e);
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -306,6 +326,87 @@ std::vector<float> transpose_cols(const std::vector<float>& W, int rows, int ld,
     for (int k = 0; k < ncols; ++k)
         for (int o = 0; o < rows; ++o) out[(size_t)k * rows + o] = W[(size_t)o * ld + col0 + k];
     return out;
+}
+
+// Persistent-engine weight layout (kernels_persist.hip). Slot w of a group, thread tid
+// (og = tid / 16, kc = tid % 16, unit u = 16 w + og % 16) holds in registers, float4 i:
+//   0..23  gate j = i / 8 of unit u, k-float4 16 (i % 8) + kc: W_ih2[:, :512] (og < 16) or
+//          W_hh1 (og >= 16)
+//   24..31 fc2 row u (og < 16) or fc1 row u (og >= 16), x part only
+//   32..39 fc3 row cpw w + og when a slot owns more than 16 classes
+// and in LDS: W_hh2 rows [16 units][3 gates][128 float4], then fc3 rows [16][128 float4].
+int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
+    auto& T = h->host;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    auto& P = h->pw;
+    P.ok = false;
+    if (h->cfg.model_type != WRNN_MODEL_FATCHORD || H != kPH || F != kPH || n > kPM * kPCls)
+        return WRNN_OK;
+    const auto& Wih2 = T["rnn2.weight_ih_l0"];  // (3H, H + A)
+    const auto& Whh1 = T["rnn1.weight_hh_l0"];  // (3H, H)
+    const auto& Whh2 = T["rnn2.weight_hh_l0"];  // (3H, H)
+    const auto& Wf1 = T["fc1.weight"];          // (F, H + A)
+    const auto& Wf2 = T["fc2.weight"];          // (F, F + A)
+    const auto& Wf3 = T["fc3.weight"];          // (n, F)
+    P.cpw = (n + kPM - 1) / kPM;
+    P.nw = persist_reg_f4(P.cpw);
+    const int nw = P.nw;
+    std::vector<float> wreg((size_t)kPM * kPT * nw * 4, 0.f);
+    std::vector<float> wlds((size_t)kPM * kPLdsW4 * 4, 0.f);
+    auto put4 = [](float* d, const float* s) { std::memcpy(d, s, 4 * sizeof(float)); };
+    for (int w = 0; w < kPM; ++w) {
+        for (int tid = 0; tid < kPT; ++tid) {
+            const int og = tid >> 4, kc = tid & 15, u = 16 * w + (og & 15);
+            float* d = wreg.data() + ((size_t)w * kPT + tid) * nw * 4;
+            for (int i = 0; i < 24; ++i) {
+                const int j = i / 8, k0 = 4 * (16 * (i % 8) + kc), row = j * H + u;
+                put4(d + 4 * i, og < 16 ? &Wih2[(size_t)row * (H + A) + k0] : &Whh1[(size_t)row * H + k0]);
+            }
+            for (int i = 24; i < 32; ++i) {
+                const int k0 = 4 * (16 * (i - 24) + kc);
+                put4(d + 4 * i, og < 16 ? &Wf2[(size_t)u * (F + A) + k0] : &Wf1[(size_t)u * (H + A) + k0]);
+            }
+            if (nw > 32) {
+                const int c = P.cpw * w + og;
+                if (og < P.cpw && c < n)
+                    for (int i = 32; i < 40; ++i)
+                        put4(d + 4 * i, &Wf3[(size_t)c * F + 4 * (16 * (i - 32) + kc)]);
+            }
+        }
+        float* L = wlds.data() + (size_t)w * kPLdsW4 * 4;
+        for (int ul = 0; ul < 16; ++ul)
+            for (int j = 0; j < 3; ++j)
+                std::memcpy(L + ((size_t)(ul * 3 + j) * kPK4) * 4,
+                            &Whh2[(size_t)(j * H + 16 * w + ul) * H], H * sizeof(float));
+        if (P.cpw <= 16)
+            for (int og = 0; og < P.cpw; ++og) {
+                const int c = P.cpw * w + og;
+                if (c < n)
+                    std::memcpy(L + ((size_t)16 * 3 * kPK4 + (size_t)og * kPK4) * 4,
+                                &Wf3[(size_t)c * F], F * sizeof(float));
+            }
+    }
+    int rc = WRNN_OK;
+    P.wreg = upload(h, wreg, &rc);
+    CHECK(rc);
+    P.wlds = upload(h, wlds, &rc);
+    CHECK(rc);
+    P.WIh1T = upload(h, transpose_cols(T["rnn1.weight_ih_l0"], 3 * H, H, 0, H), &rc);  // (H, 3H)
+    CHECK(rc);
+    auto dv = [&](const std::string& key) -> const float* {
+        if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
+        return h->dvec[key];
+    };
+    P.b_ih1 = dv("rnn1.bias_ih_l0");
+    P.b_hh1 = dv("rnn1.bias_hh_l0");
+    P.b_hh2 = dv("rnn2.bias_hh_l0");
+    P.b_fc3 = dv("fc3.bias");
+    CHECK(rc);
+    P.oG2 = oG2;
+    P.oF1 = oF1;
+    P.oF2 = oF2;
+    P.ok = true;
+    return WRNN_OK;
 }
 
 int do_finalize(wrnn_handle* h) {
@@ -491,7 +592,9 @@ int do_finalize(wrnn_handle* h) {
         s3.segs.push_back(seg_fc("fc3", n, F, SL_Y2, SL_LOG, false, dv("fc3.bias"), -1));
         CHECK(rc);
         h->stages = {s0, s1, s2, s3};
+        CHECK(pack_persist(h, oG2, oF1, oF2));
     } else {
+        h->pw.ok = false;
         const int oG3 = add_aux(1, "rnn3.weight_ih_l0", "rnn3.bias_ih_l0", 3 * H, H + A, H);
         const int oF1 = add_aux(2, "fc1.weight", "fc1.bias", F, H + A, H);
         const int oF3 = add_aux(3, "fc3.weight", "fc3.bias", F, F + A, F);
@@ -934,70 +1037,11 @@ struct UttPlan {
     int T, L, B, Lpad, pbase, fbase, row0;
 };
 
-int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
-                  int batched, int target, int overlap, int* row_offset, int* seq_len,
-                  wrnn_progress_fn cb, void* user) {
-    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
-    if (!h->finalized)
-        return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
-    if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
-    if (batched && (target <= 0 || overlap < 0))
-        return fail(WRNN_ERR_INVALID, "target must be > 0 and overlap >= 0");
-    if (!batched && n_utts != 1)
-        return fail(WRNN_ERR_INVALID, "unbatched generation takes one utterance");
-    std::vector<UttPlan> plan(n_utts);
-    int B = 0, S = 0, P = 0, Fr = 0, Tmax = 0;
-    for (int u = 0; u < n_utts; ++u) {
-        UttPlan& p = plan[u];
-        p.T = n_frames[u];
-        if (p.T <= 0) return fail(WRNN_ERR_INVALID, "mel has no frames");
-        p.L = p.T * h->hop;
-        int b, s;
-        fold_shape(p.L, batched, target, overlap, &b, &s);
-        if (b <= 0) return fail(WRNN_ERR_INVALID, "mel too short for target/overlap");
-        if (u && s != S) return fail(WRNN_ERR_INVALID, "inconsistent seq_len");
-        S = s;
-        p.B = b;
-        p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
-        p.pbase = P;
-        p.fbase = Fr;
-        p.row0 = B;
-        B += b;
-        P += p.Lpad;
-        Fr += p.T + 1;
-        Tmax = std::max(Tmax, p.T);
-    }
-    if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
-    CHECK(ensure_workspace(h, B, S, P, Fr, Tmax));
+// CHAIN engine: per step one launch per stage + the sampler, captured 100 steps per graph.
+int run_chain(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     auto& ws = h->ws;
-    h->last_B = B;
-    h->last_S = S;
-    h->last_T0 = plan[0].T;
-    h->last_L0 = plan[0].L;
+    const int B = h->last_B;
     h->RT = pick_rt(B, &h->nrt);
-    // rows
-    std::vector<RowInfo> rows(B);
-    for (int u = 0; u < n_utts; ++u) {
-        const UttPlan& p = plan[u];
-        for (int f = 0; f < p.B; ++f) {
-            RowInfo& ri = rows[p.row0 + f];
-            ri.rel0 = batched ? f * (target + overlap) : 0;
-            ri.pos0 = p.pbase + ri.rel0;
-            ri.L = p.L;
-            ri.fbase = p.fbase;
-            ri.fold = f;
-            ri.stream = h->stream_ctr + (uint32_t)u;
-        }
-        if (row_offset) row_offset[u] = p.row0;
-    }
-    if (row_offset) row_offset[n_utts] = B;
-    h->rows_host = rows;
-    HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
-                        hipMemcpyHostToDevice, h->stream));
-    // upsample + conditioning per utterance
-    for (int u = 0; u < n_utts; ++u)
-        CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, B,
-                           plan[u].row0, plan[u].fbase));
     HIPC(prepare_stage(h->stages[0].K, h->RT, h->nrg));
     {
         const char* env = std::getenv("WRNN_PHASE_STEP");
@@ -1100,17 +1144,339 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     }
     for (auto e : evs)
         if (e) (void)hipEventDestroy(e);
-    if (rc) {
-        (void)hipStreamSynchronize(h->stream);
-        return rc;
-    }
-    if (seq_len) *seq_len = S;
-    h->stream_ctr += (uint32_t)n_utts;
+    if (rc) return rc;
     if (h->phase_step >= 0) phase_report(h);
     return WRNN_OK;
 }
 
+constexpr int kPersistFallback = 1;  // internal: retry the call on the CHAIN engine
+
+bool persist_device_ok(wrnn_handle* h) {
+    static int cached[64];  // 0 unknown, 1 ok, 2 not ok (per device ordinal)
+    const int d = h->device;
+    if (d >= 0 && d < 64 && cached[d]) return cached[d] == 1;
+    hipDeviceProp_t p;
+    bool ok = hipGetDeviceProperties(&p, d) == hipSuccess && p.multiProcessorCount == kPG * kPM &&
+              std::strncmp(p.gcnArchName, "gfx950", 6) == 0 &&
+              p.sharedMemPerMultiprocessor >= persist_lds_bytes();
+    if (d >= 0 && d < 64) cached[d] = ok ? 1 : 2;
+    return ok;
+}
+
+void persist_phase_report(wrnn_handle* h, int t) {
+    std::vector<uint32_t> ph((size_t)kPG * kPM * kPPhases);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return;
+    if (hipMemcpy(ph.data(), h->pws.phases.p, ph.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+    long long t0 = -1;
+    for (int w = 0; w < kPG * kPM; ++w)
+        if (ph[(size_t)w * kPPhases] && (t0 < 0 || ph[(size_t)w * kPPhases] < t0)) t0 = ph[(size_t)w * kPPhases];
+    static const char* names[] = {"start", "A", "hopA", "B", "hopB", "C", "hopC", "D", "hopD", "sample", "gru1"};
+    std::fprintf(stderr, "[wrnn persist phases] step %d (us from the earliest start)\n", t);
+    for (int i = 0; i < 11; ++i) {
+        std::vector<double> d;
+        for (int w = 0; w < kPG * kPM; ++w) {
+            const uint32_t v = ph[(size_t)w * kPPhases + i];
+            if (v) d.push_back(((long long)v - t0) * 0.01);
+        }
+        if (d.empty()) continue;
+        std::sort(d.begin(), d.end());
+        std::fprintf(stderr, "  %-7s min %6.2f med %6.2f max %6.2f\n", names[i], d.front(), d[d.size() / 2],
+                     d.back());
+    }
+}
+
+// PERSIST engine: P1 for all steps (one MFMA GEMM), Gumbel noise (RAW), step-0 state, then
+// the persistent recurrence in chunks (one chunk per call unless a progress callback wants
+// reports; every 1000 steps then).
+int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
+    auto& ws = h->ws;
+    auto& P = h->pws;
+    const auto& W = h->pw;
+    const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;
+    const bool raw = h->cfg.mode == WRNN_MODE_RAW;
+    hipStream_t st = h->stream;
+    CHECK(P.P1.alloc((size_t)S * Bp * 3 * H * sizeof(float)));
+    if (raw) CHECK(P.gumbel.alloc((size_t)S * Bp * n * sizeof(float)));
+    CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
+    CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
+    CHECK(P.xbuf.alloc(persist_xbuf_floats() * sizeof(float)));
+    CHECK(P.st.alloc((size_t)Bp * 6 * H * sizeof(float)));
+    // P1[t][r] = W_ih1 cI[t][r] + b_ih1
+    {
+        GemmA ga{};
+        GemmB gb{};
+        GemmEp ge{};
+        ga.kind = 0;
+        ga.p = ws.cI.f();
+        ga.ld = H;
+        gb.kind = 0;
+        gb.p = W.WIh1T;
+        gb.ld = 3 * H;
+        ge.kind = 0;
+        ge.D = P.P1.f();
+        ge.ld = 3 * H;
+        ge.bias = W.b_ih1;
+        HIPC(launch_gemm(S * Bp, 3 * H, H, ga, gb, ge, st));
+    }
+    const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
+    if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, (const RowInfo*)ws.rows.p, k0, k1, st));
+    PersistArgs a{};
+    a.ctl = (unsigned*)P.ctl.p;
+    a.flags = (unsigned*)P.flags.p;
+    a.xbuf = P.xbuf.f();
+    a.S = S;
+    a.B = Bp;
+    a.nr = Bp / kPG;
+    a.mode = h->cfg.mode;
+    a.n_classes = n;
+    a.hop = h->hop;
+    a.cpw = W.cpw;
+    a.rows = (const RowInfo*)ws.rows.p;
+    a.wreg = (const float4*)W.wreg;
+    a.wlds = (const float4*)W.wlds;
+    a.b_hh1 = W.b_hh1;
+    a.b_hh2 = W.b_hh2;
+    a.b_fc3 = W.b_fc3;
+    a.v = h->v1;
+    a.w0 = h->w0;
+    a.fcond = ws.fcond.f();
+    a.cond_width = h->cond_width;
+    a.oG2 = W.oG2;
+    a.oF1 = W.oF1;
+    a.oF2 = W.oF2;
+    a.P1 = P.P1.f();
+    a.cI = ws.cI.f();
+    a.gumbel = raw ? P.gumbel.f() : nullptr;
+    a.labels = (int16_t*)ws.labels.p;
+    a.samples = ws.samples.f();
+    a.ld = ws.S;
+    a.k0 = k0;
+    a.k1 = k1;
+    a.st_x1 = P.st.f();
+    a.st_h1 = a.st_x1 + (size_t)Bp * H;
+    a.st_h2 = a.st_h1 + (size_t)Bp * H;
+    a.st_gh2 = a.st_h2 + (size_t)Bp * H;
+    a.phase_t = -1;
+    if (const char* env = std::getenv("WRNN_PHASE_STEP")) {
+        a.phase_t = std::min(std::atoi(env), S - 1);
+        CHECK(P.phases.alloc((size_t)kPG * kPM * kPPhases * sizeof(uint32_t)));
+        HIPC(hipMemsetAsync(P.phases.p, 0, P.phases.bytes, st));
+        a.phases = (uint32_t*)P.phases.p;
+    }
+    HIPC(launch_persist_init(a, st));
+    HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
+    HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
+    const int G = cb ? 1000 : S;
+    const int nchunks = (S + G - 1) / G;
+    for (auto e : h->pev) (void)hipEventDestroy(e);
+    h->pev.clear();
+    h->pev_steps.clear();
+    if (h->timing) CHECK(P.stamps.alloc((size_t)nchunks * 2 * sizeof(uint32_t)));
+    const auto t_start = std::chrono::steady_clock::now();
+    std::vector<hipEvent_t> done(nchunks, nullptr);
+    int rc = WRNN_OK;
+    for (int c = 0; c < nchunks && rc == WRNN_OK; ++c) {
+        a.t0 = c * G;
+        a.t1 = std::min(S, a.t0 + G);
+        // registration words only: an error code from an earlier chunk stays visible
+        HIPC(hipMemsetAsync(P.ctl.p, 0, PC_ERR * sizeof(unsigned), st));
+        a.stamps = h->timing ? (uint32_t*)P.stamps.p + 2 * c : nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            HIPC(hipEventCreate(&e0));
+            HIPC(hipEventCreate(&e1));
+            h->pev.push_back(e0);
+            h->pev.push_back(e1);
+            h->pev_steps.push_back(a.t1 - a.t0);
+            HIPC(hipEventRecord(e0, st));
+        }
+        HIPC(launch_persist(a, st));
+        if (h->timing) HIPC(hipEventRecord(e1, st));
+        if (cb) {
+            if (hipEventCreateWithFlags(&done[c], hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(done[c], st) != hipSuccess) {
+                rc = fail(WRNN_ERR_HIP, "event record");
+                break;
+            }
+            if (c >= 1) {  // report the previous chunk (one chunk stays queued ahead)
+                (void)hipEventSynchronize(done[c - 1]);
+                const int i = a.t0 - G;
+                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+                if (cb(user, i, S, B, (i + 1) / std::max(el, 1e-9) * B / 1000.0))
+                    rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+            }
+        }
+    }
+    if (rc == WRNN_OK && cb) {
+        (void)hipEventSynchronize(done[nchunks - 1]);
+        const int i = (nchunks - 1) * G;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        if (cb(user, i, S, B, (i + 1) / std::max(el, 1e-9) * B / 1000.0))
+            rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+    }
+    for (auto e : done)
+        if (e) (void)hipEventDestroy(e);
+    if (rc) return rc;
+    unsigned err = 0;
+    HIPC(hipMemcpyAsync(&err, (unsigned*)P.ctl.p + PC_ERR, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (err) {
+        static const char* what[] = {"", "workgroups did not become co-resident",
+                                     "exchange timeout", "workgroups not spread 32 per XCD"};
+        fail(WRNN_ERR_HIP, std::string("persistent launch: ") + (err < 4 ? what[err] : "unknown error"));
+        return kPersistFallback;
+    }
+    if (a.phase_t >= 0) persist_phase_report(h, a.phase_t);
+    // algorithmic traffic per step: recurrent weights once + per row-step
+    // conditioning (mel 80 + aux 128 floats) and the label
+    double wparams = 0;
+    for (const char* k : {"I.weight", "I.bias", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn1.bias_ih_l0",
+                          "rnn1.bias_hh_l0", "rnn2.weight_ih_l0", "rnn2.weight_hh_l0", "rnn2.bias_ih_l0",
+                          "rnn2.bias_hh_l0", "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias",
+                          "fc3.weight", "fc3.bias"})
+        wparams += (double)h->host[k].size();
+    h->p_step_bytes = 4.0 * wparams + B * ((h->feat + h->R) * 4.0 + 2.0);
+    double macs = 0;
+    for (const char* k : {"I.weight", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn2.weight_ih_l0",
+                          "rnn2.weight_hh_l0", "fc1.weight", "fc2.weight", "fc3.weight"})
+        macs += (double)h->host[k].size();
+    h->p_step_flops = 2.0 * macs * B;
+    return WRNN_OK;
+}
+
+int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
+                  int batched, int target, int overlap, int* row_offset, int* seq_len,
+                  wrnn_progress_fn cb, void* user) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (!h->finalized)
+        return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
+    if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
+    if (batched && (target <= 0 || overlap < 0))
+        return fail(WRNN_ERR_INVALID, "target must be > 0 and overlap >= 0");
+    if (!batched && n_utts != 1)
+        return fail(WRNN_ERR_INVALID, "unbatched generation takes one utterance");
+    std::vector<UttPlan> plan(n_utts);
+    int B = 0, S = 0, P = 0, Fr = 0, Tmax = 0;
+    for (int u = 0; u < n_utts; ++u) {
+        UttPlan& p = plan[u];
+        p.T = n_frames[u];
+        if (p.T <= 0) return fail(WRNN_ERR_INVALID, "mel has no frames");
+        p.L = p.T * h->hop;
+        int b, s;
+        fold_shape(p.L, batched, target, overlap, &b, &s);
+        if (b <= 0) return fail(WRNN_ERR_INVALID, "mel too short for target/overlap");
+        if (u && s != S) return fail(WRNN_ERR_INVALID, "inconsistent seq_len");
+        S = s;
+        p.B = b;
+        p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
+        p.pbase = P;
+        p.fbase = Fr;
+        p.row0 = B;
+        B += b;
+        P += p.Lpad;
+        Fr += p.T + 1;
+        Tmax = std::max(Tmax, p.T);
+    }
+    if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
+    // engine: PERSIST when asked for / automatic and the call qualifies
+    int want = h->engine;
+    if (const char* env = std::getenv("WRNN_ENGINE")) {
+        if (!std::strcmp(env, "chain")) want = WRNN_ENGINE_CHAIN;
+        else if (!std::strcmp(env, "persist")) want = WRNN_ENGINE_PERSIST;
+        else if (!std::strcmp(env, "auto")) want = WRNN_ENGINE_AUTO;
+    }
+    std::string why;
+    const int nr = (B + kPG - 1) / kPG;
+    bool use_p = false;
+    if (want != WRNN_ENGINE_CHAIN) {
+        if (!h->pw.ok) why = "model is not fatchord with rnn_dims = fc_dims = 512 and <= 1024 classes";
+        else if (B > kPG * kPNR) why = std::to_string(B) + " fold rows > " + std::to_string(kPG * kPNR);
+        else if (!persist_variant_ok(nr, h->pw.cpw)) why = "no register-resident variant for this row count";
+        else if (h->persist_failed) why = "a persistent launch failed earlier on this handle";
+        else if (!persist_device_ok(h)) why = "device is not a 256-CU gfx950";
+        else use_p = true;
+        if (want == WRNN_ENGINE_PERSIST && !use_p)
+            return fail(WRNN_ERR_INVALID, "persist engine unavailable: " + why);
+    }
+    const int Bp = use_p ? kPG * nr : B;  // persistent groups carry nr rows each
+    CHECK(ensure_workspace(h, Bp, S, P, Fr, Tmax));
+    auto& ws = h->ws;
+    h->last_B = B;
+    h->last_Bp = Bp;
+    h->last_S = S;
+    h->last_T0 = plan[0].T;
+    h->last_L0 = plan[0].L;
+    // rows (pad rows repeat the last real row's addressing; their outputs are never read)
+    std::vector<RowInfo> rows(Bp);
+    for (int u = 0; u < n_utts; ++u) {
+        const UttPlan& p = plan[u];
+        for (int f = 0; f < p.B; ++f) {
+            RowInfo& ri = rows[p.row0 + f];
+            ri.rel0 = batched ? f * (target + overlap) : 0;
+            ri.pos0 = p.pbase + ri.rel0;
+            ri.L = p.L;
+            ri.fbase = p.fbase;
+            ri.fold = f;
+            ri.stream = h->stream_ctr + (uint32_t)u;
+        }
+        if (row_offset) row_offset[u] = p.row0;
+    }
+    for (int r = B; r < Bp; ++r) rows[r] = rows[B - 1];
+    if (row_offset) row_offset[n_utts] = B;
+    h->rows_host = rows;
+    HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
+                        hipMemcpyHostToDevice, h->stream));
+    // upsample + conditioning per utterance (cI folded with row stride Bp)
+    for (int u = 0; u < n_utts; ++u)
+        CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
+                           plan[u].row0, plan[u].fbase));
+    int rc = WRNN_OK;
+    if (use_p) {
+        rc = run_persist(h, S, cb, user);
+        if (rc == kPersistFallback) {
+            // the persistent launch could not run (e.g. CUs unavailable): same call on CHAIN
+            std::fprintf(stderr, "[wavernn-mi355x] persist engine failed (%s); using the chain engine\n",
+                         g_err.c_str());
+            h->persist_failed = true;
+            use_p = false;
+            h->last_B = Bp;  // chain runs every padded row (cI stride is Bp)
+            rc = run_chain(h, S, cb, user);
+            h->last_B = B;
+        }
+    } else {
+        rc = run_chain(h, S, cb, user);
+    }
+    if (rc) {
+        (void)hipStreamSynchronize(h->stream);
+        return rc;
+    }
+    h->last_engine = use_p ? WRNN_ENGINE_PERSIST : WRNN_ENGINE_CHAIN;
+    if (seq_len) *seq_len = S;
+    h->stream_ctr += (uint32_t)n_utts;
+    return WRNN_OK;
+}
+
 int collect_timing(wrnn_handle* h) {
+    if (h->last_engine == WRNN_ENGINE_PERSIST) {
+        // one stage: HIP-event duration of each persistent launch on its own stream
+        h->stage_avg_us.assign(1, 0.0);
+        h->stage_launches.assign(1, 0);
+        h->p_avg_steps = 0;
+        if (!h->timing || h->pev.empty()) return WRNN_OK;
+        HIPC(hipStreamSynchronize(h->stream));
+        double tot = 0, steps = 0;
+        const int nl = (int)h->pev.size() / 2;
+        for (int i = 0; i < nl; ++i) {
+            float ms = 0;
+            HIPC(hipEventElapsedTime(&ms, h->pev[2 * i], h->pev[2 * i + 1]));
+            tot += ms * 1000.0;
+            steps += h->pev_steps[i];
+        }
+        h->stage_avg_us[0] = tot / nl;
+        h->stage_launches[0] = nl;
+        h->p_avg_steps = steps / nl;
+        return WRNN_OK;
+    }
     const int ns = (int)h->stages.size();
     h->stage_avg_us.assign(ns, 0.0);
     h->stage_launches.assign(ns, 0);
@@ -1348,9 +1714,33 @@ int wrnn_stage_timing(wrnn_handle* h, int stage, double* avg_us, int* launches) 
     return WRNN_OK;
 }
 
+int wrnn_set_engine(wrnn_handle* h, int engine) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (engine != WRNN_ENGINE_AUTO && engine != WRNN_ENGINE_CHAIN && engine != WRNN_ENGINE_PERSIST)
+        return fail(WRNN_ERR_INVALID, "unknown engine " + std::to_string(engine));
+    h->engine = engine;
+    return WRNN_OK;
+}
+
+int wrnn_last_engine(wrnn_handle* h, int* engine) {
+    if (!h || !engine) return fail(WRNN_ERR_INVALID, "null argument");
+    *engine = h->last_engine;
+    return WRNN_OK;
+}
+
 int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, double* bytes,
                     double* flops, int* n_stages) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (h->last_engine == WRNN_ENGINE_PERSIST) {
+        if (n_stages) *n_stages = 1;
+        if (stage != 0) return fail(WRNN_ERR_INVALID, "bad stage index");
+        if (name && name_cap) std::snprintf(name, name_cap, "%s", "persist");
+        // per launch = steps per launch x per-step algorithmic bytes / FLOPs
+        const double steps = h->p_avg_steps > 0 ? h->p_avg_steps : h->last_S;
+        if (bytes) *bytes = steps * h->p_step_bytes;
+        if (flops) *flops = steps * h->p_step_flops;
+        return WRNN_OK;
+    }
     if (n_stages) *n_stages = (int)h->stages.size();
     if (stage < 0 || stage >= (int)h->stages.size())
         return fail(WRNN_ERR_INVALID, "bad stage index");

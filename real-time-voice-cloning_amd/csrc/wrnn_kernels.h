@@ -142,4 +142,70 @@ hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, f
                               int ld_out, hipStream_t s);
 hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------
+// Persistent, weight-stationary fatchord recurrence (kernels_persist.hip). 8 XCD-local groups
+// of 32 workgroups; group g owns fold rows g, g+8, ... g+8(NR-1) (the host pads the row count
+// to 8*NR so every group carries the same number of rows).
+// ---------------------------------------------------------------------------------------
+constexpr int kPG = 8;       // groups (one per XCD)
+constexpr int kPM = 32;      // workgroups per group
+constexpr int kPT = 512;     // threads per workgroup
+constexpr int kPNR = 4;      // max fold rows per group -> B <= 32
+constexpr int kPH = 512;     // rnn_dims == fc_dims
+constexpr int kPK4 = kPH / 4;
+constexpr int kPCls = 32;    // max classes per workgroup -> n_classes <= 1024
+constexpr int kPPhases = 12; // diagnostic stamps per workgroup per traced step
+
+// float4 weight registers per thread: 24 gate rows (stage A) + 8 fc1|fc2 rows [+ 8 fc3 rows
+// when a workgroup owns more than 16 classes]; the rest of the slot's weights live in LDS.
+inline int persist_reg_f4(int cpw) { return cpw > 16 ? 40 : 32; }
+// LDS weights per slot (float4): W_hh2 [16 units][3][kPK4], then fc3 [16 classes][kPK4]
+constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
+
+// control words (zeroed by the host before every launch); PC_ERR: 1 registration timeout,
+// 2 exchange timeout, 3 workgroups not spread 32 per XCD
+enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WORDS = 16 };
+
+struct PersistArgs {
+    unsigned* ctl;          // PC_WORDS control words
+    unsigned* flags;        // [kPG][4 hops][64]; monotonic step counters within one call
+    float* xbuf;            // per-group exchange area (persist_xbuf_floats())
+    int t0, t1, S;          // steps [t0, t1) of S
+    int B, nr;              // padded rows (= 8 * nr)
+    int mode, n_classes, hop, cpw;  // cpw = classes per workgroup
+    const RowInfo* rows;    // [B]
+    const float4* wreg;     // [kPM][kPT][persist_reg_f4(cpw)]
+    const float4* wlds;     // [kPM][kPLdsW4]
+    const float* b_hh1;     // [3H]
+    const float* b_hh2;     // [3H]
+    const float* b_fc3;     // [n]
+    const float* v;         // [3H] W_ih1 . w0
+    const float* w0;        // [H]
+    const float* fcond;     // per-frame conditioning rows
+    int cond_width, oG2, oF1, oF2;
+    const float* P1;        // [S][B][3H] = W_ih1 cI + b_ih1
+    const float* cI;        // [S][B][H]
+    const float* gumbel;    // [S][B][n] (RAW)
+    int16_t* labels;        // [B][ld]
+    float* samples;         // [B][ld]
+    int ld;
+    uint32_t k0, k1;        // Philox key (MOL draws in-kernel)
+    float* st_x1;           // [B][H] chunk state: x1, h1 of step t0 ...
+    float* st_h1;
+    float* st_h2;           // ... h2 and gh2 = W_hh2 h2 + b_hh2 after step t0-1
+    float* st_gh2;          // [B][3H]
+    uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
+    uint32_t* phases;       // optional: [256][kPPhases] stamps of step phase_t
+    int phase_t;
+};
+
+hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
+hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
+hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
+                         uint32_t k0, uint32_t k1, hipStream_t s);
+int persist_variant_ok(int nr, int cpw);
+size_t persist_lds_bytes();
+size_t persist_xbuf_floats();
+size_t persist_flag_words();
+
 }  // namespace wrnn

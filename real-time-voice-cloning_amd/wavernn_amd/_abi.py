@@ -23,11 +23,17 @@ WRNN_MODEL_RUNTIMERACER = 1
 WRNN_MODE_RAW = 0
 WRNN_MODE_MOL = 1
 
+WRNN_ENGINE_AUTO = 0
+WRNN_ENGINE_CHAIN = 1
+WRNN_ENGINE_PERSIST = 2
+ENGINES = {'auto': WRNN_ENGINE_AUTO, 'chain': WRNN_ENGINE_CHAIN, 'persist': WRNN_ENGINE_PERSIST}
+
 EXPORTED = [
     'wrnn_version', 'wrnn_last_error', 'wrnn_device_count', 'wrnn_create', 'wrnn_destroy',
     'wrnn_load_tensor', 'wrnn_finalize', 'wrnn_set_seed', 'wrnn_set_stream', 'wrnn_fold_shape',
     'wrnn_generate', 'wrnn_generate_batch_device', 'wrnn_enable_stage_timing',
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
+    'wrnn_set_engine', 'wrnn_last_engine',
 ]
 
 
@@ -62,6 +68,13 @@ def load_library(path=None):
             f'{LIB_NAME} not found at {path}: build it with `make -C '
             f'real-time-voice-cloning_amd/csrc` or __graft_entry__.build(); the MI355X vocoder '
             f'has no CPU fallback')
+    try:
+        # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7
+        # must be loaded first so this library binds to it (same SONAME) instead of pulling
+        # in /opt/rocm's copy, after which torch.cuda cannot initialise.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P = ctypes.POINTER
     c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
@@ -83,6 +96,8 @@ def load_library(path=None):
         'wrnn_generate_batch_device': (c_int, [c_void_p, c_int, P(c_void_p), P(c_int), c_int,
                                                c_int, c_int, c_void_p, c_void_p, c_size_t,
                                                P(c_int), P(c_int), PROGRESS_FN, c_void_p]),
+        'wrnn_set_engine': (c_int, [c_void_p, c_int]),
+        'wrnn_last_engine': (c_int, [c_void_p, P(c_int)]),
         'wrnn_enable_stage_timing': (c_int, [c_void_p, c_int]),
         'wrnn_stage_timing': (c_int, [c_void_p, c_int, P(ctypes.c_double), P(c_int)]),
         'wrnn_stage_info': (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t,

@@ -136,6 +136,18 @@ class WaveRNN:
                                              ctypes.byref(b), ctypes.byref(s)))
         return b.value, s.value
 
+    def set_engine(self, engine):
+        """'auto' (default), 'chain' or 'persist' for later calls (include/wavernn_mi355x.h)."""
+        if engine not in _abi.ENGINES:
+            raise ValueError(f'unknown engine {engine!r}; expected one of {sorted(_abi.ENGINES)}')
+        _abi.check(self._lib.wrnn_set_engine(self._h, _abi.ENGINES[engine]))
+
+    def last_engine(self):
+        """Engine ('chain' or 'persist') that ran the last call."""
+        e = ctypes.c_int()
+        _abi.check(self._lib.wrnn_last_engine(self._h, ctypes.byref(e)))
+        return {v: k for k, v in _abi.ENGINES.items()}[e.value]
+
     def enable_stage_timing(self, enable=True):
         _abi.check(self._lib.wrnn_enable_stage_timing(self._h, int(bool(enable))))
 

@@ -28,14 +28,17 @@ def make_model(meta):
     return m, hp, sd
 
 
-def run_case(name):
+def run_case(name, engine='auto'):
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
     meta, gold = golden_case(name)
     m, hp, sd = make_model(meta)
+    m.set_engine(engine)
     mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
     wav = m.generate(mel[None], meta['batched'], meta['target'], meta['overlap'], hp.mu_law,
                      sp.preemphasize, progress_callback=lambda *a: None)
+    if engine != 'auto':
+        assert m.last_engine() == engine
     return meta, gold, m, wav
 
 
@@ -44,25 +47,37 @@ def first_divergence(a, b):
     return None if len(d) == 0 else tuple(d[np.argmin(d[:, 1])])
 
 
-RAW_CASES = [k for k, v in golden_meta().items() if v['mode'] == 'RAW']
-MOL_CASES = [k for k, v in golden_meta().items() if v['mode'] == 'MOL']
+def engine_cases(mode):
+    # CHAIN runs every topology; PERSIST runs fatchord (rnn_dims = fc_dims = 512)
+    out = []
+    for k, v in golden_meta().items():
+        if v['mode'] != mode:
+            continue
+        out.append((k, 'chain'))
+        if v['model_type'] == 'fatchord-wavernn':
+            out.append((k, 'persist'))
+    return out
 
 
-@pytest.mark.parametrize('name', RAW_CASES)
-def test_raw_labels_and_wave_bit_exact(name):
-    meta, gold, m, wav = run_case(name)
+RAW_CASES = engine_cases('RAW')
+MOL_CASES = engine_cases('MOL')
+
+
+@pytest.mark.parametrize('name,engine', RAW_CASES)
+def test_raw_labels_and_wave_bit_exact(name, engine):
+    meta, gold, m, wav = run_case(name, engine)
     lab = m.last_labels
     assert lab.shape == gold['labels'].shape == (meta['num_folds'], meta['seq_len'])
     agree = float((lab == gold['labels']).mean())
-    assert agree == 1.0, f'{name}: label agreement {agree}, first divergence (row, step) ' \
+    assert agree == 1.0, f'{name}/{engine}: label agreement {agree}, first divergence (row, step) ' \
                          f'{first_divergence(lab, gold["labels"])}'
     assert wav.dtype == np.float64 and wav.shape == gold['wav'].shape
     assert np.array_equal(wav, gold['wav'])
 
 
-@pytest.mark.parametrize('name', MOL_CASES)
-def test_mol_float_path_within_tolerance(name):
-    meta, gold, m, wav = run_case(name)
+@pytest.mark.parametrize('name,engine', MOL_CASES)
+def test_mol_float_path_within_tolerance(name, engine):
+    meta, gold, m, wav = run_case(name, engine)
     s = m.last_samples
     rms = float(np.sqrt(np.mean((s.astype(np.float64) - gold['samples']) ** 2)))
     rms_w = float(np.sqrt(np.mean((wav - gold['wav']) ** 2)))
@@ -100,3 +115,32 @@ def test_upsample_network_matches_oracle():
     ref_mel = ref_mel[0].numpy().T
     np.testing.assert_allclose(aux, ref_aux, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('n_utts', [3, 4, 6])
+def test_persist_multi_row_groups_match_oracle(n_utts):
+    """5 fold rows per utterance -> 15 / 20 / 30 rows: 2, 3 and 4 rows per XCD group (the
+    padded-row variants of the persistent engine), every row against the oracle."""
+    import torch
+    from oracle.wavernn_oracle import oracle_infer_waveform
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_raw9_sharp_tiny')
+    m, hp, sd = make_model(meta)
+    mels = [synth_mel(meta['n_frames'], 100 + u) / sp.max_abs_value for u in range(n_utts)]
+    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
+    m.set_engine('persist')
+    m.set_seed(meta['noise_seed'])
+    try:
+        lab, row_off, S = m.generate_batch_device(dev, True, meta['target'], meta['overlap'])
+    except ValueError as e:  # no spill-free variant for this row count on this build
+        pytest.skip(str(e))
+    assert m.last_engine() == 'persist'
+    lab = lab.cpu().numpy()
+    for u in range(n_utts):
+        ref = oracle_infer_waveform(sd, hp, meta['model_type'], mels[u] * sp.max_abs_value,
+                                    target=meta['target'], overlap=meta['overlap'],
+                                    seed=meta['noise_seed'], stream=u)
+        got = lab[row_off[u]:row_off[u + 1]]
+        assert np.array_equal(got, ref['labels']), \
+            f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'

@@ -2,7 +2,7 @@
 # Print VGPR / spill / LDS / occupancy per kernel of a HIP source (compile-time remarks).
 f=${1:-kernels_step.hip}
 cd "$(dirname "$0")/../real-time-voice-cloning_amd/csrc"
-/opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -I../../include -c "$f" -o /tmp/ru.o \
+/opt/rocm/bin/hipcc -std=c++17 -O3 -fno-slp-vectorize --offload-arch=gfx950 -I../../include -c "$f" -o /tmp/ru.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import sys, re
 cur = None
