@@ -103,7 +103,11 @@ constexpr int L_X0 = 0;                             // [kPNR][512]
 constexpr int L_X1 = L_X0 + kPNR * kPH;             // [kPNR][512]
 constexpr int L_RED = L_X1 + kPNR * kPH;            // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
-constexpr int L_W = L_SX + 16;                      // slot weights (kPLdsW4 float4)
+constexpr int L_CNT = L_SX + 8;                     // producer counters of the publishes
+constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
+constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
+constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
+constexpr int L_W = L_RI + 28;                      // slot weights (kPLdsW4 float4)
 constexpr int L_FC3 = L_W + 16 * 3 * kPH;           // fc3 rows inside the weight block
 constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 
@@ -140,6 +144,32 @@ __device__ __forceinline__ void p_publish(unsigned* flag, unsigned value, int ti
     __syncthreads();
     if (tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+template <int CTRL>
+__device__ __forceinline__ int pdpp_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp_step(float& v, int& k) {
+    const float v2 = pdpp<CTRL>(v);
+    const int k2 = pdpp_i<CTRL>(k);
+    if (v2 > v || (v2 == v && k2 < k)) {
+        v = v2;
+        k = k2;
+    }
+}
+// argmax over the 16 lanes of a DPP row (value, class); ties -> lowest class; all lanes get it
+__device__ __forceinline__ void row16_argmax(float& v, int& k) {
+    amax_dpp_step<0xB1>(v, k);
+    amax_dpp_step<0x4E>(v, k);
+    amax_dpp_step<0x124>(v, k);
+    amax_dpp_step<0x128>(v, k);
+}
+
+// RAW hop D carries its own sequence tag: each slot writes one 64-bit word per row,
+// (value bits, step << 11 | class), so consumers poll the candidates themselves.
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+constexpr unsigned kTagSeqMask = (1u << 21) - 1;  // steps per call < 2^21 (host-checked)
 
 // argmax over the 32 lanes of a half-wave (value, class); ties -> lowest class
 __device__ __forceinline__ void half_argmax(float& v, int& k) {
@@ -219,8 +249,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * XB_GROUP);  // this group's exchange area
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
-#define PSTAMP(i) \
-    if (trace && t == a.phase_t && tid == 0) ph[i] = p_now()
+    // stamps of wave 0 at [i], of wave 4 at [12 + i]; shader-clock cycles of the traced step
+    // (wave 0) at [24] / [25] give the core clock against the 100 MHz stamps
+#define PSTAMP(i)                                                        \
+    if (trace && t == a.phase_t && (tid & 255) == 0) {                   \
+        ph[(tid >> 8) * 12 + (i)] = p_now();                             \
+        if (tid == 0 && ((i) == 0 || (i) == 10))                         \
+            ph[24 + ((i) == 10)] = (uint32_t)__builtin_amdgcn_s_memtime(); \
+    }
 
     // ---- weights: registers and LDS -----------------------------------------------------
     constexpr int NW = FC3R ? 40 : 32;
@@ -236,7 +272,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     }
     // ---- chunk state -----------------------------------------------------------------------
     // thread tid = unit j of the redundant GRU1; lanes kc < NR of og < 16 own (u, row kc) of GRU2
-    float h1[NR], h2r = 0.f, gh2r[3] = {0.f, 0.f, 0.f};
+    float h1[NR], h2r = 0.f;
     const bool own = gate_a && kc < NR;
     const int lr = kc < NR ? kc : 0;
     const int lrow = g + kPG * lr;  // row of this lane's epilogue
@@ -250,19 +286,21 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     if (own) {
         h2r = a.st_h2[(size_t)lrow * H + u];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) gh2r[j] = a.st_gh2[(size_t)lrow * 3 * H + j * H + u];
+        for (int j = 0; j < 3; ++j)
+            lds[L_GH2 + (og * 3 + j) * kPNR + kc] = a.st_gh2[(size_t)lrow * 3 * H + j * H + u];
     }
     // per-thread constants
     const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid], w0j = a.w0[tid];
     float b3[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) b3[j] = gate_a ? a.b_hh2[j * H + u] : a.b_hh1[j * H + u];
+    for (int j = 0; j < 3; ++j) b3[j] = gate_a ? 0.f : a.b_hh1[j * H + u];
     const float bcls = has_cls ? a.b_fc3[cls] : 0.f;
-    const RowInfo lri = a.rows[lrow];
+    float bh2[3];  // waves 4-7 compute gh2 of unit u (stage C)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) bh2[j] = gate_a ? 0.f : a.b_hh2[j * H + u];
+    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g + kPG * tid];
     // per-lane byte offsets (32-bit)
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
-    const unsigned o_P1 = (unsigned)(g * 3 * H + tid) * 4u;             // P1 row g, unit tid
-    const unsigned o_cI = (unsigned)(g * H + tid) * 4u;                 // cI row g, unit tid
     const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 4u;             // bufA row lr, unit u
     const unsigned o_y = (unsigned)(lr * kPH + u) * 4u;                 // bufB/C row lr, unit u
     const unsigned o_gum = (unsigned)(lrow * a.n_classes + cls) * 4u;   // gumbel row lrow
@@ -273,30 +311,33 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
 
     const float4* X0 = reinterpret_cast<const float4*>(lds + L_X0);
     const float4* X1 = reinterpret_cast<const float4*>(lds + L_X1);
-    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
-    for (int t = a.t0; t < a.t1; ++t) {
-        const unsigned seq = (unsigned)t + 1u;
-        const unsigned sA = (unsigned)(XB_A + (t & 1) * XB_A_SZ) * 4u;  // bufA of this step
-        PSTAMP(0);
-        // ---- per-step inputs, issued now, consumed at the epilogues / GRU1 ------------------
-        float pP[NR][3], pC[NR];
-        const bool nxt = t + 1 < a.S;
+    unsigned* cnt = reinterpret_cast<unsigned*>(lds + L_CNT);  // producer counters per hop
+    const int wave = tid >> 6;
+    const bool wv_lo = wave < 4;  // waves 0-3: og < 16 (GRU2, hh2, fc2, fc3 <= 16 classes)
+    // Per-step operands, issued right after the wave's last publish of the previous step
+    // (waves 0-3: hop C, waves 4-7: hop B) so the publish never waits on them:
+    //   pP/pC  P1(tg+1), cI(tg+1) of this thread's GRU1 unit   (end of step tg)
+    //   pc*    per-frame conditioning of step te's epilogues  (stages A-C of step te)
+    //   pgn    Gumbel noise of step te, class cls            (stage D of step te)
+    float pP[NR][3], pC[NR];
+    float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f, pgn = 0.f;
+    auto prefetch = [&](int tg, int te) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) pP[r][0] = pP[r][1] = pP[r][2] = pC[r] = 0.f;
-        if (nxt) {
-            const rsrc_t pr = mk_rsrc(a.P1 + (size_t)(t + 1) * a.B * 3 * H);
-            const rsrc_t cr = mk_rsrc(a.cI + (size_t)(t + 1) * a.B * H);
+        if (tg + 1 < a.S) {
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(tg + 1) * a.B + g) * 3 * H);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(tg + 1) * a.B + g) * H);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j)
-                    pP[r][j] = bld(pr, o_P1, (unsigned)(r * kPG * 3 * H + j * H) * 4u);
-                pC[r] = bld(cr, o_cI, (unsigned)(r * kPG * H) * 4u);
+                    pP[r][j] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * H + j * H) * 4u);
+                pC[r] = bld(cr, o_tid, (unsigned)(r * kPG * H) * 4u);
             }
         }
-        float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f;
-        if (kc < NR) {
-            const unsigned fo = (unsigned)(p_frame(lri, t, a.hop) * a.cond_width) * 4u;
+        if (kc < NR && te < a.S) {
+            const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
+            const unsigned fo = (unsigned)(p_frame(lri, te, a.hop) * a.cond_width) * 4u;
             pc0 = bld(fcr, o_fc + fo, 0);
             if (gate_a) {
                 pc1 = bld(fcr, o_fc + fo, H * 4);
@@ -304,32 +345,74 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pf2 = bld(fcr, o_f2 + fo, 0);
             }
             if (has_cls && a.mode == 0)
-                pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes), o_gum, 0);
+                pgn = bld(mk_rsrc(a.gumbel + (size_t)te * a.B * a.n_classes), o_gum, 0);
         }
-        // ================= stage A: GRU2 (og<16) | W_hh1 h1 (og>=16) =================
-        {
-            v2f acc[3][NR];
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-#pragma unroll
-                for (int r = 0; r < NR; ++r) acc[j][r] = (v2f){0.f, 0.f};
-            const float4* Xs = gate_a ? X0 : X1;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const float4 x4 = Xs[r * kPK4 + 16 * q + kc];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) dot4(acc[j][r], wr[j * 8 + q], x4);
-                }
+    };
+    // L2 warm-up of step tt's streamed inputs (P1, cI, Gumbel rows of this group), one line
+    // per load, spread over the group's 32 workgroups; issued by waves 4-7 after their
+    // publish so no exchange waits on them.
+    const int lines_g = a.mode == 0 ? a.n_classes / 32 : 1;
+    const int lines_r = 48 + 16 + lines_g;
+    float tacc = 0.f;
+    auto touch = [&](int tt) {
+        const int i = tid - 256;
+        const int li = w + kPM * i;
+        if (tt >= a.S || i < 0 || li >= NR * lines_r) return;
+        const int r = li / lines_r, l = li % lines_r, row = g + kPG * r;
+        if (l < 48)
+            tacc += bld(mk_rsrc(a.P1 + ((size_t)tt * a.B + row) * 3 * H), (unsigned)l * 128u, 0);
+        else if (l < 64)
+            tacc += bld(mk_rsrc(a.cI + ((size_t)tt * a.B + row) * H), (unsigned)(l - 48) * 128u, 0);
+        else
+            tacc += bld(mk_rsrc(a.gumbel + ((size_t)tt * a.B + row) * (a.mode == 0 ? a.n_classes : kMolNoise)),
+                        (unsigned)(l - 64) * 128u, 0);
+    };
+    // publish by the producer waves only: each waits for its own stores, the last one to
+    // arrive (LDS counter) stores the flag
+    auto publish_by = [&](unsigned* flag, unsigned value, unsigned* c, unsigned nprod) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((tid & 63) == 0) {
+            const unsigned old = atomicAdd(c, 1u);
+            if (old == nprod - 1) {
+                *c = 0u;
+                __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+        }
+    };
+    if (tid < 4) cnt[tid] = 0u;
+    if (tid == 0) lds[L_FAIL] = 0.f;
+    prefetch(a.t0, a.t0);
+    pgum = pgn;
+    touch(a.t0 + 1);
+    __syncthreads();
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
+    for (int t = a.t0; t < a.t1; ++t) {
+        const unsigned seq = (unsigned)t + 1u;
+        const unsigned sA = (unsigned)(XB_A + (t & 1) * XB_A_SZ) * 4u;  // bufA of this step
+        const bool nxt = t + 1 < a.S;
+        PSTAMP(0);
+        // ================= stage A: GRU2 (waves 0-3, critical) | W_hh1 h1 (waves 4-7) =======
+        if (wv_lo) __builtin_amdgcn_s_setprio(2);
+        {
+            const float4* Xs = gate_a ? X0 : X1;
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const float t0 = row16_sum(hsum(acc[0][r]));
-                const float t1 = row16_sum(hsum(acc[1][r]));
-                const float t2 = row16_sum(hsum(acc[2][r]));
+            for (int r = 0; r < NR; ++r) {  // weights are register-resident: row-outer
+                v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
+#pragma unroll
+                for (int qb = 0; qb < 8; qb += 4) {  // LDS loads in batches of 4 (latency)
+                    __builtin_amdgcn_sched_barrier(0);
+                    float4 xq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) xq[q] = Xs[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) dot4(acc[j], wr[j * 8 + qb + q], xq[q]);
+                }
+                const float t0 = row16_sum(hsum(acc[0]));
+                const float t1 = row16_sum(hsum(acc[1]));
+                const float t2 = row16_sum(hsum(acc[2]));
                 if (kc == r) {
                     s0 = t0;
                     s1 = t1;
@@ -338,37 +421,103 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
             if (kc < NR) {
                 if (gate_a) {
+                    const float* gh2 = lds + L_GH2 + og * 3 * kPNR + kc;
                     const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2),
-                                           gh2r[0], gh2r[1], gh2r[2], h2r);
+                                           gh2[0], gh2[kPNR], gh2[2 * kPNR], h2r);
                     h2r = hn;
                     bst(p_add(lds[L_X0 + lr * kPH + u], hn), xr, o_u, sA);  // x2 = x1 + h2
                     bst(hn, xr, o_u, sA + kPH * 4);
-                } else {
+                } else {  // gh1 for GRU1 at the end of this step: published with hop B
                     bst(p_add(s0, b3[0]), xr, o_u, sA + 2 * kPH * 4);
                     bst(p_add(s1, b3[1]), xr, o_u, sA + 3 * kPH * 4);
                     bst(p_add(s2, b3[2]), xr, o_u, sA + 4 * kPH * 4);
                 }
             }
         }
+        if (wv_lo) {
+            publish_by(fl + 0 * 64 + w, seq, cnt + 0, 4);
+            __builtin_amdgcn_s_setprio(0);
+        }
         PSTAMP(1);
-        p_publish(fl + 0 * 64 + w, seq, tid);
         if (!p_wait(fl + 0 * 64, seq, a.ctl, tid)) return;
         PSTAMP(2);
-        // ================= stage B: fc1 (og>=16) | W_hh2 h2 (og<16, LDS weights) ======
-        for (int i = tid; i < NR * kPK4; i += kPT) {
-            const int r = i / kPK4, q = i % kPK4;
-            const unsigned o = (unsigned)(r * 5 * kPH + 4 * q) * 4u;
-            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, o, sA);
-            reinterpret_cast<float4*>(lds + L_X1)[i] = bld4_nt(xr, o, sA + kPH * 4);
+        // ================= stage B: fc1 (waves 4-7) ==========================================
+        if (wv_lo) {
+            for (int i = tid; i < NR * kPK4; i += 256) {
+                const int r = i / kPK4, q = i % kPK4;
+                const unsigned o = (unsigned)(r * 5 * kPH + 4 * q) * 4u;
+                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, o, sA);
+                reinterpret_cast<float4*>(lds + L_X1)[i] = bld4_nt(xr, o, sA + kPH * 4);
+            }
         }
         __syncthreads();
-        if (gate_a) {
+        if (!gate_a) {
+            __builtin_amdgcn_s_setprio(2);
+            float s0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                v2f acc = {0.f, 0.f};
+#pragma unroll
+                for (int qb = 0; qb < 8; qb += 4) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    float4 xq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dot4(acc, wr[24 + qb + q], xq[q]);
+                }
+                const float t0 = row16_sum(hsum(acc));
+                if (kc == r) s0 = t0;
+            }
+            if (kc < NR) {
+                const float y = p_add(s0, pc0);
+                bst(y > 0.f ? y : 0.f, xr, o_y, XB_B * 4);
+            }
+            publish_by(fl + 1 * 64 + w, seq, cnt + 1, 4);  // also covers gh1 of stage A
+            __builtin_amdgcn_s_setprio(0);
+            touch(t + 2);
+        }
+        PSTAMP(3);
+        if (!p_wait(fl + 1 * 64, seq, a.ctl, tid)) return;
+        PSTAMP(4);
+        // ================= stage C: fc2 (waves 0-3, critical) | W_hh2 h2 (waves 4-7) ========
+        if (wv_lo) {
+            for (int i = tid; i < NR * kPK4; i += 256)
+                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_B * 4);
+        }
+        __syncthreads();
+        if (wv_lo) {
+            __builtin_amdgcn_s_setprio(2);
+            float s0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                v2f acc = {0.f, 0.f};
+#pragma unroll
+                for (int qb = 0; qb < 8; qb += 4) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    float4 xq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dot4(acc, wr[24 + qb + q], xq[q]);
+                }
+                const float t0 = row16_sum(hsum(acc));
+                if (kc == r) s0 = t0;
+            }
+            if (kc < NR) {
+                const float y = p_add(s0, pf2);
+                bst(y > 0.f ? y : 0.f, xr, o_y, XB_C * 4);
+            }
+            publish_by(fl + 2 * 64 + w, seq, cnt + 2, 4);
+            __builtin_amdgcn_s_setprio(0);
+        } else {
+            // off the critical path: gh2 = W_hh2 h2 + b_hh2 for the next step's GRU2
             v2f acc[3][NR];
 #pragma unroll
             for (int j = 0; j < 3; ++j)
 #pragma unroll
                 for (int r = 0; r < NR; ++r) acc[j][r] = (v2f){0.f, 0.f};
-            const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)og * 3 * kPK4;
+            const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)(og - 16) * 3 * kPK4;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -394,94 +543,54 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     s2 = t2;
                 }
             }
-            if (kc < NR) {  // gh2 for the next step stays in this lane
-                gh2r[0] = p_add(s0, b3[0]);
-                gh2r[1] = p_add(s1, b3[1]);
-                gh2r[2] = p_add(s2, b3[2]);
-            }
-        } else {
-            v2f acc[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) dot4(acc[r], wr[24 + q], X0[r * kPK4 + 16 * q + kc]);
-            }
-            float s0 = 0.f;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const float t0 = row16_sum(hsum(acc[r]));
-                if (kc == r) s0 = t0;
-            }
-            if (kc < NR) {
-                const float y = p_add(s0, pc0);
-                bst(y > 0.f ? y : 0.f, xr, o_y, XB_B * 4);
-            }
-        }
-        PSTAMP(3);
-        p_publish(fl + 1 * 64 + w, seq, tid);
-        if (!p_wait(fl + 1 * 64, seq, a.ctl, tid)) return;
-        PSTAMP(4);
-        // ================= stage C: fc2 (og<16) ============================================
-        for (int i = tid; i < NR * kPK4; i += kPT)
-            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_B * 4);
-        __syncthreads();
-        if (gate_a) {
-            v2f acc[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) dot4(acc[r], wr[24 + q], X0[r * kPK4 + 16 * q + kc]);
-            }
-            float s0 = 0.f;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const float t0 = row16_sum(hsum(acc[r]));
-                if (kc == r) s0 = t0;
-            }
-            if (kc < NR) {
-                const float y = p_add(s0, pf2);
-                bst(y > 0.f ? y : 0.f, xr, o_y, XB_C * 4);
+            if (kc < NR) {  // gh2 for the next step's GRU2
+                float* gh2 = lds + L_GH2 + (og - 16) * 3 * kPNR + kc;
+                gh2[0] = p_add(s0, bh2[0]);
+                gh2[kPNR] = p_add(s1, bh2[1]);
+                gh2[2 * kPNR] = p_add(s2, bh2[2]);
             }
         }
         PSTAMP(5);
-        p_publish(fl + 2 * 64 + w, seq, tid);
         if (!p_wait(fl + 2 * 64, seq, a.ctl, tid)) return;
         PSTAMP(6);
-        // ================= stage D: fc3 -> candidates =======================================
-        float pG[NR][3];  // gh1 of GRU1(t+1) (published at hop A)
+        // ================= stage D: fc3 -> per-slot candidates (wave 0 publishes) ===========
+        // GRU1 operands (gh1 published with hop B; P1 / cI L2-warm) and the next step's
+        // epilogue operands: waves 1-7 now, wave 0 after it publishes hop D
+        float pG[NR][3];
+        auto load_gh1 = [&]() {
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
+            for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
-                pG[r][j] = bld_nt(xr, o_tid, sA + (unsigned)(r * 5 * kPH + (2 + j) * kPH) * 4u);
-        for (int i = tid; i < NR * kPK4; i += kPT)
-            reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_C * 4);
+                for (int j = 0; j < 3; ++j)
+                    pG[r][j] = bld_nt(xr, o_tid, sA + (unsigned)(r * 5 * kPH + (2 + j) * kPH) * 4u);
+        };
+        if (wv_lo) {
+            for (int i = tid; i < NR * kPK4; i += 256)
+                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_C * 4);
+        }
         __syncthreads();
         {
-            v2f acc[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+            float s0 = 0.f;
             if (has_cls) {
                 const float4* Wf = reinterpret_cast<const float4*>(lds + L_FC3) + (size_t)og * kPK4;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    const float4 w4 = FC3R ? wr[(32 + q) % NW] : Wf[16 * q + kc];
+                for (int r = 0; r < NR; ++r) {
+                    v2f acc = {0.f, 0.f};
 #pragma unroll
-                    for (int r = 0; r < NR; ++r) dot4(acc[r], w4, X0[r * kPK4 + 16 * q + kc]);
+                    for (int qb = 0; qb < 8; qb += 4) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        float4 xq[4], wq[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+                            wq[q] = FC3R ? wr[(32 + qb + q) % NW] : Wf[16 * (qb + q) + kc];
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) dot4(acc, wq[q], xq[q]);
+                    }
+                    const float t0 = row16_sum(hsum(acc));
+                    if (kc == r) s0 = t0;
                 }
-            }
-            float s0 = 0.f;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const float t0 = row16_sum(hsum(acc[r]));
-                if (kc == r) s0 = t0;
             }
             float* red = lds + L_RED;  // [og][r][value, class]
             if (kc < NR) {
@@ -490,41 +599,82 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     const float l = p_add(s0, bcls);
                     if (a.mode == 0)
                         val = p_add(l, pgum);
-                    else  // MOL: logits row
+                    else  // MOL: logits row (og == 0 -> wave 0)
                         bst(l, xr, (unsigned)(kc * 64 + cls) * 4u, (XB_D + XB_D_LOG) * 4);
                 }
                 red[(og * kPNR + kc) * 2] = val;
                 red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
             }
             __syncthreads();
-            if (a.mode == 0 && tid < NR) {
-                const int r = tid;
-                float bv = -INFINITY;
-                int bi = 0x7fffffff;
-                for (int o = 0; o < a.cpw; ++o) {
-                    const float v2 = red[(o * kPNR + r) * 2];
-                    const int i2 = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
-                    if (v2 > bv || (v2 == bv && i2 < bi)) {
-                        bv = v2;
-                        bi = i2;
+            if (wave == 0) {
+                if (a.mode == 0) {
+                    // slot candidate per row, tagged with the step (no flag, no wait)
+                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
+                        const int r = tid >> 4, o = tid & 15;
+                        float bv = -INFINITY;
+                        int bi = 0x7fffffff;
+                        if (r < NR && o < a.cpw) {
+                            bv = red[(o * kPNR + r) * 2];
+                            bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                        }
+                        row16_argmax(bv, bi);
+                        if (r < NR && o == 0)
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                (unsigned)((w * kPNR + r) * 2) * 4u, XB_D * 4, 0);
+                    } else {
+#pragma unroll
+                        for (int rb = 0; rb < NR; rb += 2) {
+                            const int r = rb + (tid >> 5), o = tid & 31;
+                            float bv = -INFINITY;
+                            int bi = 0x7fffffff;
+                            if (r < NR && o < a.cpw) {
+                                bv = red[(o * kPNR + r) * 2];
+                                bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                            }
+                            half_argmax(bv, bi);
+                            if (r < NR && o == 0)
+                                __builtin_amdgcn_raw_buffer_store_b64(
+                                    (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                    (unsigned)((w * kPNR + r) * 2) * 4u, XB_D * 4, 0);
+                        }
                     }
+                } else {  // MOL: logits rows + flag
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (tid == 0)
+                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                const unsigned o = (unsigned)((w * kPNR + r) * 2) * 4u;
-                bst(bv, xr, o, XB_D * 4);
-                bst(__int_as_float(bi), xr, o + 4, XB_D * 4);
             }
         }
+        load_gh1();
+        prefetch(t, t + 1);
+        pgum = pgn;
         PSTAMP(7);
-        p_publish(fl + 3 * 64 + w, seq, tid);
-        if (!p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
+        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
         PSTAMP(8);
         // ================= sample of step t (redundant in every workgroup) ==================
         if (a.mode == 0) {
-            if (tid < 32 * NR) {  // half-wave r: lane o holds slot o's candidate
+            if (tid < 32 * NR) {  // half-wave r: lane o polls slot o's tagged candidate of row r
                 const int r = tid >> 5, o = tid & 31;
                 const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
-                float bv = bld_nt(xr, off, XB_D * 4);
-                int bi = __float_as_int(bld_nt(xr, off + 4, XB_D * 4));
+                const unsigned want = seq & kTagSeqMask;
+                u2v c;
+                const unsigned t0 = p_now();
+                unsigned n = 0;
+                while (true) {
+                    c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
+                    if (__all((c.y >> 11) == want)) break;
+                    if ((++n & 255) == 0) {
+                        if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
+                            if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                            lds[L_FAIL] = 1.f;
+                            break;
+                        }
+                    }
+                }
+                float bv = __uint_as_float(c.x);
+                int bi = (int)(c.y & 0x7ffu);
                 half_argmax(bv, bi);
                 if (o == 0) {
                     float xv;
@@ -534,55 +684,49 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     }
                     lds[L_SX + r] = xv;
                     if (w == 0) {
-                        const int row = g + kPG * r;
-                        a.labels[(size_t)row * a.ld + t] = (int16_t)bi;
-                        a.samples[(size_t)row * a.ld + t] = xv;
+                        const unsigned ro = (unsigned)((g + kPG * r) * a.ld);
+                        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
+                                                              ro * 2u, (unsigned)t * 2u, 0);
+                        bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
                     }
                 }
             }
         } else if (tid < NR) {
-            // MOL: vocoder/distribution.py:104-140 with the Philox draws (kernels_step.hip)
+            // MOL: vocoder/distribution.py:104-140; the Philox draws were turned into
+            // gm_k = log(-log(u1_k)) and lu = log(u2) - log(1 - u2) by k_mol_noise
             const int r = tid, row = g + kPG * r;
-            const RowInfo ri = a.rows[row];
             const unsigned lo = (unsigned)(r * 64) * 4u;
             const unsigned so = (XB_D + XB_D_LOG) * 4;
-            uint32_t wd[11];
+            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
+            float gm[11];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const U4 o4 = philox4x32_10(kMolDomain | (uint32_t)j, (uint32_t)t, (uint32_t)ri.fold,
-                                            ri.stream, a.k0, a.k1);
-                wd[4 * j] = o4.x;
-                wd[4 * j + 1] = o4.y;
-                wd[4 * j + 2] = o4.z;
-                if (j < 2) wd[4 * j + 3] = o4.w;
-            }
+            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
             float xv;
             {
 #pragma clang fp contract(off)
                 float bv = -INFINITY;
                 int bi = 0;
+#pragma unroll
                 for (int k = 0; k < 10; ++k) {
-                    const float u1 = mol_uniform_from_u32(wd[k]);
-                    const float v2 = bld_nt(xr, lo + 4u * k, so) - logf(-logf(u1));
+                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
                     if (v2 > bv) {
                         bv = v2;
                         bi = k;
                     }
                 }
-                const float u2 = mol_uniform_from_u32(wd[10]);
                 const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
                 float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
                 const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
                 ls = ls < lsmin ? lsmin : ls;
-                const float lu = logf(u2) - logf(1.0f - u2);
-                xv = mean + expf(ls) * lu;
+                xv = mean + expf(ls) * gm[10];
                 xv = xv < -1.f ? -1.f : xv;
                 xv = xv > 1.f ? 1.f : xv;
             }
             lds[L_SX + r] = xv;
-            if (w == 0) a.samples[(size_t)row * a.ld + t] = xv;
+            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
         }
         __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
         PSTAMP(9);
         if (!nxt) continue;
         // ================= GRU1 of step t+1 for all 512 units (redundant) ===================
@@ -596,6 +740,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X0 + r * kPH + tid] = p_add(fmaf(w0j, x, pC[r]), hn);
             lds[L_X1 + r * kPH + tid] = hn;
         }
+        asm volatile("" ::"v"(tacc));  // the L2 warm-up loads retire here at the latest
         __syncthreads();
         PSTAMP(10);
     }
@@ -613,7 +758,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         if (own) {
             a.st_h2[(size_t)lrow * H + u] = h2r;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) a.st_gh2[(size_t)lrow * 3 * H + j * H + u] = gh2r[j];
+            for (int j = 0; j < 3; ++j)
+                a.st_gh2[(size_t)lrow * 3 * H + j * H + u] = lds[L_GH2 + (og * 3 + j) * kPNR + kc];
         }
     }
 }
@@ -664,6 +810,43 @@ hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInf
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gumbel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        reinterpret_cast<float4*>(g), S, nrows, ng, rows, k0, k1);
+    return hipGetLastError();
+}
+
+// MOL noise of the RNG contract (philox.h, oracle/philox.py mol_uniforms) in the form the
+// sampler consumes, with the sampler's own float operations (kernels_step.hip k_sample):
+// [k < 10] = log(-log(u1_k)), [10] = log(u2) - log(1 - u2), [11] = 0.
+__global__ __launch_bounds__(256) void k_mol_noise(float* out, int S, int nrows, const RowInfo* rows,
+                                                   uint32_t k0, uint32_t k1) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r)
+    if (i >= (size_t)S * nrows) return;
+    const int r = (int)(i % nrows), t = (int)(i / nrows);
+    const RowInfo ri = rows[r];
+    uint32_t wd[12];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const U4 o = philox4x32_10(kMolDomain | (uint32_t)j, (uint32_t)t, (uint32_t)ri.fold, ri.stream, k0, k1);
+        wd[4 * j] = o.x;
+        wd[4 * j + 1] = o.y;
+        wd[4 * j + 2] = o.z;
+        wd[4 * j + 3] = o.w;
+    }
+    float* d = out + i * kMolNoise;
+    {
+#pragma clang fp contract(off)
+        for (int k = 0; k < 10; ++k) d[k] = logf(-logf(mol_uniform_from_u32(wd[k])));
+        const float u2 = mol_uniform_from_u32(wd[10]);
+        d[10] = logf(u2) - logf(1.0f - u2);
+        d[11] = 0.f;
+    }
+}
+
+hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, uint32_t k0,
+                            uint32_t k1, hipStream_t s) {
+    const size_t total = (size_t)S * nrows;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mol_noise, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, S,
+                       nrows, rows, k0, k1);
     return hipGetLastError();
 }
 

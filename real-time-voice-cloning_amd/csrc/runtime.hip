@@ -172,8 +172,9 @@ struct wrnn_handle {
     struct PersistW {
         bool ok = false;  // weights packed: fatchord, rnn_dims = fc_dims = 512, n <= 1024
         int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;
-        const float *wreg = nullptr, *wlds = nullptr, *WIh1T = nullptr;
-        const float *b_ih1 = nullptr, *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;
+        const float *wreg = nullptr, *wlds = nullptr;
+        const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
+        const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;
     } pw;
     struct PersistWS {
         DevBuf P1, gumbel, ctl, flags, xbuf, st, stamps, phases;
@@ -391,13 +392,40 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     CHECK(rc);
     P.wlds = upload(h, wlds, &rc);
     CHECK(rc);
-    P.WIh1T = upload(h, transpose_cols(T["rnn1.weight_ih_l0"], 3 * H, H, 0, H), &rc);  // (H, 3H)
-    CHECK(rc);
+    // P1 = W_ih1 (I[:,1:] c + b_I) + b_ih1 = M1 c + bP1 with M1 = W_ih1 I[:,1:] (f64 products):
+    // one K = feat + A - 1 contraction per (step, row) instead of K = rnn_dims
+    {
+        const auto& Wih1 = T["rnn1.weight_ih_l0"];  // (3H, H)
+        const auto& WI = T["I.weight"];             // (H, feat + A)
+        const auto& bI = T["I.bias"];
+        const auto& bih1 = T["rnn1.bias_ih_l0"];
+        const int ldI = h->feat + A, KI = h->KI;
+        std::vector<double> WIk((size_t)H * KI);
+        for (int j = 0; j < H; ++j)
+            for (int k = 0; k < KI; ++k) WIk[(size_t)j * KI + k] = WI[(size_t)j * ldI + 1 + k];
+        std::vector<float> M1T((size_t)KI * 3 * H), bP1(3 * H);
+        std::vector<double> acc(KI);
+        for (int o = 0; o < 3 * H; ++o) {
+            std::fill(acc.begin(), acc.end(), 0.0);
+            double b = bih1[o];
+            for (int j = 0; j < H; ++j) {
+                const double wv = Wih1[(size_t)o * H + j];
+                const double* row = &WIk[(size_t)j * KI];
+                for (int k = 0; k < KI; ++k) acc[k] += wv * row[k];
+                b += wv * (double)bI[j];
+            }
+            for (int k = 0; k < KI; ++k) M1T[(size_t)k * 3 * H + o] = (float)acc[k];
+            bP1[o] = (float)b;
+        }
+        P.M1T = upload(h, M1T, &rc);
+        CHECK(rc);
+        P.bP1 = upload(h, bP1, &rc);
+        CHECK(rc);
+    }
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
     };
-    P.b_ih1 = dv("rnn1.bias_ih_l0");
     P.b_hh1 = dv("rnn1.bias_hh_l0");
     P.b_hh2 = dv("rnn2.bias_hh_l0");
     P.b_fc3 = dv("fc3.bias");
@@ -705,7 +733,7 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
 
 // ---- upsample network + conditioning for one utterance --------------------------------
 int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
-                 int row0, int fbase) {
+                 int row0, int fbase, float* P1out) {
     auto& ws = h->ws;
     hipStream_t st = h->stream;
     const int C = h->C, R = h->R, H = h->H;
@@ -835,6 +863,14 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         e4.Btot = Btot;
         e4.row0 = row0;
         HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
+        if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
+            b4.p = h->pw.M1T;
+            b4.ld = 3 * H;
+            e4.D = P1out;
+            e4.ld = 3 * H;
+            e4.bias = h->pw.bP1;
+            HIPC(launch_gemm(S * Bu, 3 * H, h->KI, a4, b4, e4, st));
+        }
     }
     // per-frame aux conditioning, slot 0 = zero frame
     for (const auto& ac : h->auxc) {
@@ -1164,24 +1200,41 @@ bool persist_device_ok(wrnn_handle* h) {
 }
 
 void persist_phase_report(wrnn_handle* h, int t) {
+    // per group: the last workgroup to reach each phase (the group's critical path), relative
+    // to the group's first start; printed as the median and max over the 8 groups
     std::vector<uint32_t> ph((size_t)kPG * kPM * kPPhases);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return;
     if (hipMemcpy(ph.data(), h->pws.phases.p, ph.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
-    long long t0 = -1;
-    for (int w = 0; w < kPG * kPM; ++w)
-        if (ph[(size_t)w * kPPhases] && (t0 < 0 || ph[(size_t)w * kPPhases] < t0)) t0 = ph[(size_t)w * kPPhases];
     static const char* names[] = {"start", "A", "hopA", "B", "hopB", "C", "hopC", "D", "hopD", "sample", "gru1"};
-    std::fprintf(stderr, "[wrnn persist phases] step %d (us from the earliest start)\n", t);
+    std::fprintf(stderr, "[wrnn persist phases] step %d: last workgroup of each group, us from the group's first start"
+                         " (wave 0 | wave 4)\n", t);
     for (int i = 0; i < 11; ++i) {
-        std::vector<double> d;
-        for (int w = 0; w < kPG * kPM; ++w) {
-            const uint32_t v = ph[(size_t)w * kPPhases + i];
-            if (v) d.push_back(((long long)v - t0) * 0.01);
+        double med[2] = {0, 0}, mxx[2] = {0, 0};
+        for (int wv = 0; wv < 2; ++wv) {
+            std::vector<double> d;
+            for (int g = 0; g < kPG; ++g) {
+                long long t0 = -1, mx = -1;
+                for (int w = 0; w < kPM; ++w) {
+                    const uint32_t s0 = ph[((size_t)g * kPM + w) * kPPhases];
+                    const uint32_t v = ph[((size_t)g * kPM + w) * kPPhases + 12 * wv + i];
+                    if (s0 && (t0 < 0 || s0 < t0)) t0 = s0;
+                    if (v && (long long)v > mx) mx = v;
+                }
+                if (t0 >= 0 && mx >= 0) d.push_back((mx - t0) * 0.01);
+            }
+            if (d.empty()) continue;
+            std::sort(d.begin(), d.end());
+            med[wv] = d[d.size() / 2];
+            mxx[wv] = d.back();
         }
-        if (d.empty()) continue;
-        std::sort(d.begin(), d.end());
-        std::fprintf(stderr, "  %-7s min %6.2f med %6.2f max %6.2f\n", names[i], d.front(), d[d.size() / 2],
-                     d.back());
+        std::fprintf(stderr, "  %-7s med %6.2f max %6.2f | med %6.2f max %6.2f\n", names[i], med[0], mxx[0], med[1],
+                     mxx[1]);
+    }
+    {
+        // core clock of workgroup 0: shader cycles / 100 MHz ticks over the traced step
+        const double cyc = (double)(uint32_t)(ph[25] - ph[24]);
+        const double us = ((long long)ph[10] - (long long)ph[0]) * 0.01;
+        if (us > 0) std::fprintf(stderr, "  shader clock ~ %.0f MHz\n", cyc / us);
     }
 }
 
@@ -1195,31 +1248,15 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;
     const bool raw = h->cfg.mode == WRNN_MODE_RAW;
     hipStream_t st = h->stream;
-    CHECK(P.P1.alloc((size_t)S * Bp * 3 * H * sizeof(float)));
-    if (raw) CHECK(P.gumbel.alloc((size_t)S * Bp * n * sizeof(float)));
+    CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
     CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
     CHECK(P.xbuf.alloc(persist_xbuf_floats() * sizeof(float)));
     CHECK(P.st.alloc((size_t)Bp * 6 * H * sizeof(float)));
-    // P1[t][r] = W_ih1 cI[t][r] + b_ih1
-    {
-        GemmA ga{};
-        GemmB gb{};
-        GemmEp ge{};
-        ga.kind = 0;
-        ga.p = ws.cI.f();
-        ga.ld = H;
-        gb.kind = 0;
-        gb.p = W.WIh1T;
-        gb.ld = 3 * H;
-        ge.kind = 0;
-        ge.D = P.P1.f();
-        ge.ld = 3 * H;
-        ge.bias = W.b_ih1;
-        HIPC(launch_gemm(S * Bp, 3 * H, H, ga, gb, ge, st));
-    }
+    // P1 (all steps, rows) was written by run_upsample next to cI
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
     if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, (const RowInfo*)ws.rows.p, k0, k1, st));
+    else HIPC(launch_mol_noise(P.gumbel.f(), S, Bp, (const RowInfo*)ws.rows.p, k0, k1, st));
     PersistArgs a{};
     a.ctl = (unsigned*)P.ctl.p;
     a.flags = (unsigned*)P.flags.p;
@@ -1246,7 +1283,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     a.oF2 = W.oF2;
     a.P1 = P.P1.f();
     a.cI = ws.cI.f();
-    a.gumbel = raw ? P.gumbel.f() : nullptr;
+    a.gumbel = P.gumbel.f();
     a.labels = (int16_t*)ws.labels.p;
     a.samples = ws.samples.f();
     a.ld = ws.S;
@@ -1265,6 +1302,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     }
     HIPC(launch_persist_init(a, st));
     HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
+    HIPC(hipMemsetAsync(P.xbuf.p, 0, persist_xbuf_floats() * sizeof(float), st));  // step tags
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
     const int G = cb ? 1000 : S;
     const int nchunks = (S + G - 1) / G;
@@ -1393,6 +1431,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         else if (B > kPG * kPNR) why = std::to_string(B) + " fold rows > " + std::to_string(kPG * kPNR);
         else if (!persist_variant_ok(nr, h->pw.cpw)) why = "no register-resident variant for this row count";
         else if (h->persist_failed) why = "a persistent launch failed earlier on this handle";
+        else if (S >= (1 << 21)) why = "seq_len >= 2^21 (step tags)";
         else if (!persist_device_ok(h)) why = "device is not a 256-CU gfx950";
         else use_p = true;
         if (want == WRNN_ENGINE_PERSIST && !use_p)
@@ -1427,9 +1466,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
                         hipMemcpyHostToDevice, h->stream));
     // upsample + conditioning per utterance (cI folded with row stride Bp)
+    if (use_p) CHECK(h->pws.P1.alloc((size_t)S * Bp * 3 * kPH * sizeof(float)));
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
-                           plan[u].row0, plan[u].fbase));
+                           plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr));
     int rc = WRNN_OK;
     if (use_p) {
         rc = run_persist(h, S, cb, user);

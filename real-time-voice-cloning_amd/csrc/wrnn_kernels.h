@@ -154,7 +154,7 @@ constexpr int kPNR = 4;      // max fold rows per group -> B <= 32
 constexpr int kPH = 512;     // rnn_dims == fc_dims
 constexpr int kPK4 = kPH / 4;
 constexpr int kPCls = 32;    // max classes per workgroup -> n_classes <= 1024
-constexpr int kPPhases = 12; // diagnostic stamps per workgroup per traced step
+constexpr int kPPhases = 32; // diagnostic stamps per workgroup per traced step
 
 // float4 weight registers per thread: 24 gate rows (stage A) + 8 fc1|fc2 rows [+ 8 fc3 rows
 // when a workgroup owns more than 16 classes]; the rest of the slot's weights live in LDS.
@@ -185,7 +185,7 @@ struct PersistArgs {
     int cond_width, oG2, oF1, oF2;
     const float* P1;        // [S][B][3H] = W_ih1 cI + b_ih1
     const float* cI;        // [S][B][H]
-    const float* gumbel;    // [S][B][n] (RAW)
+    const float* gumbel;    // RAW [S][B][n] Gumbel noise; MOL [S][B][kMolNoise]
     int16_t* labels;        // [B][ld]
     float* samples;         // [B][ld]
     int ld;
@@ -201,6 +201,9 @@ struct PersistArgs {
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
+constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
+hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, uint32_t k0,
+                            uint32_t k1, hipStream_t s);
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
                          uint32_t k0, uint32_t k1, hipStream_t s);
 int persist_variant_ok(int nr, int cpw);
