@@ -171,16 +171,16 @@ __device__ __forceinline__ void row16_argmax(float& v, int& k) {
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 constexpr unsigned kTagSeqMask = (1u << 21) - 1;  // steps per call < 2^21 (host-checked)
 
-// argmax over the 32 lanes of a half-wave (value, class); ties -> lowest class
+// argmax over the 32 lanes of a half-wave (value, class); ties -> lowest class. DPP only:
+// each 16-lane row reduces itself, then row_bcast:15 hands row 0's (row 2's) result to row 1
+// (row 3). The half-wave's result is valid in its upper 16 lanes (lane & 31 >= 16).
 __device__ __forceinline__ void half_argmax(float& v, int& k) {
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) {
-        const float v2 = __shfl_xor(v, m, 32);
-        const int k2 = __shfl_xor(k, m, 32);
-        if (v2 > v || (v2 == v && k2 < k)) {
-            v = v2;
-            k = k2;
-        }
+    row16_argmax(v, k);
+    const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x142, 0xA, 0xF, false));
+    const int k2 = __builtin_amdgcn_update_dpp(k, k, 0x142, 0xA, 0xF, false);
+    if (v2 > v || (v2 == v && k2 < k)) {
+        v = v2;
+        k = k2;
     }
 }
 
@@ -353,19 +353,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // publish so no exchange waits on them.
     const int lines_g = a.mode == 0 ? a.n_classes / 32 : 1;
     const int lines_r = 48 + 16 + lines_g;
-    float tacc = 0.f;
+    float tv = 0.f;  // result of this thread's warm-up load; consumed at the end of the step
     auto touch = [&](int tt) {
         const int i = tid - 256;
         const int li = w + kPM * i;
         if (tt >= a.S || i < 0 || li >= NR * lines_r) return;
         const int r = li / lines_r, l = li % lines_r, row = g + kPG * r;
         if (l < 48)
-            tacc += bld(mk_rsrc(a.P1 + ((size_t)tt * a.B + row) * 3 * H), (unsigned)l * 128u, 0);
+            tv = bld(mk_rsrc(a.P1 + ((size_t)tt * a.B + row) * 3 * H), (unsigned)l * 128u, 0);
         else if (l < 64)
-            tacc += bld(mk_rsrc(a.cI + ((size_t)tt * a.B + row) * H), (unsigned)(l - 48) * 128u, 0);
+            tv = bld(mk_rsrc(a.cI + ((size_t)tt * a.B + row) * H), (unsigned)(l - 48) * 128u, 0);
         else
-            tacc += bld(mk_rsrc(a.gumbel + ((size_t)tt * a.B + row) * (a.mode == 0 ? a.n_classes : kMolNoise)),
-                        (unsigned)(l - 64) * 128u, 0);
+            tv = bld(mk_rsrc(a.gumbel + ((size_t)tt * a.B + row) * (a.mode == 0 ? a.n_classes : kMolNoise)),
+                     (unsigned)(l - 64) * 128u, 0);
     };
     // publish by the producer waves only: each waits for its own stores, the last one to
     // arrive (LDS counter) stores the flag
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                                 bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                             }
                             half_argmax(bv, bi);
-                            if (r < NR && o == 0)
+                            if (r < NR && o == 31)
                                 __builtin_amdgcn_raw_buffer_store_b64(
                                     (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
                                     (unsigned)((w * kPNR + r) * 2) * 4u, XB_D * 4, 0);
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 float bv = __uint_as_float(c.x);
                 int bi = (int)(c.y & 0x7ffu);
                 half_argmax(bv, bi);
-                if (o == 0) {
+                if (o == 31) {
                     float xv;
                     {
 #pragma clang fp contract(off)
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X0 + r * kPH + tid] = p_add(fmaf(w0j, x, pC[r]), hn);
             lds[L_X1 + r * kPH + tid] = hn;
         }
-        asm volatile("" ::"v"(tacc));  // the L2 warm-up loads retire here at the latest
+        asm volatile("" ::"v"(tv));  // the L2 warm-up load retires here at the latest
         __syncthreads();
         PSTAMP(10);
     }
