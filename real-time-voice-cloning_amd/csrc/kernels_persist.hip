@@ -87,13 +87,15 @@ __device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
     return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
 }
 
-// exchange area per group (floats): A double-buffered [r][x2 | h2 | gh1(3H)], B y1, C y2, D
+// exchange area per group (floats). A, B, C hold tagged pairs (value bits, step + 1), so a
+// consumer polls the payload itself -- no flags: A double-buffered [r][x2 | h2 | gh1 r,z,n][512],
+// B y1 [r][512], C y2 [r][512]; D the per-slot candidates (RAW, tagged) / MOL logits.
 constexpr int XB_A = 0;
-constexpr int XB_A_SZ = kPNR * 5 * kPH;
+constexpr int XB_A_SZ = kPNR * 5 * kPH * 2;
 constexpr int XB_B = XB_A + 2 * XB_A_SZ;
-constexpr int XB_C = XB_B + kPNR * kPH;
-constexpr int XB_D = XB_C + kPNR * kPH;
-constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][value, class]
+constexpr int XB_C = XB_B + kPNR * kPH * 2;
+constexpr int XB_D = XB_C + kPNR * kPH * 2;
+constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][value, tag]
 constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
 constexpr int XB_GROUP = XB_D + XB_D_SZ + 64;
 
@@ -103,13 +105,14 @@ constexpr int L_X0 = 0;                             // [kPNR][512]
 constexpr int L_X1 = L_X0 + kPNR * kPH;             // [kPNR][512]
 constexpr int L_RED = L_X1 + kPNR * kPH;            // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
-constexpr int L_CNT = L_SX + 8;                     // producer counters of the publishes
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
-constexpr int L_W = L_RI + 28;                      // slot weights (kPLdsW4 float4)
+constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
+constexpr int L_W = L_BIAS + 100;                   // slot weights (kPLdsW4 float4)
 constexpr int L_FC3 = L_W + 16 * 3 * kPH;           // fc3 rows inside the weight block
 constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
+static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 
 __device__ __forceinline__ bool p_wait(const unsigned* f, unsigned target, unsigned* ctl, int tid) {
     // wave 0 polls the group's 32 flags; every wave then meets at the barrier
@@ -204,6 +207,34 @@ __device__ __forceinline__ void bst(float v, rsrc_t r, unsigned voff, unsigned s
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
 }
 
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bst_tag(float v, unsigned tag, rsrc_t r, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(v), tag}, r, voff, soff, 0);
+}
+// Poll M 16-byte couples (two tagged pairs each) until every tag equals `want`, storing the
+// values to LDS (dst[m], float2) on every pass; the last pass, the one that saw all tags, wins.
+// False on an abort / timeout (error code set).
+template <int M>
+__device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M], unsigned so,
+                                             unsigned want, float2* const (&dst)[M], unsigned* ctl) {
+    const unsigned t0 = p_now();
+    unsigned n = 0;
+    while (true) {
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off[m], so, kCpNT);
+            *dst[m] = make_float2(__uint_as_float(c.x), __uint_as_float(c.z));
+            ok = ok && c.y == want && c.w == want;
+        }
+        if (__all(ok)) return true;
+        if ((++n & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
+            if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
+            return false;
+        }
+    }
+}
+
 template <int NR, bool FC3R>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -291,18 +322,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     }
     // per-thread constants
     const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid], w0j = a.w0[tid];
-    float b3[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) b3[j] = gate_a ? 0.f : a.b_hh1[j * H + u];
+    if (tid < 96) lds[L_BIAS + tid] = (tid < 48 ? a.b_hh1 : a.b_hh2)[(tid % 48 / 16) * H + 16 * w + (tid & 15)];
     const float bcls = has_cls ? a.b_fc3[cls] : 0.f;
-    float bh2[3];  // waves 4-7 compute gh2 of unit u (stage C)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) bh2[j] = gate_a ? 0.f : a.b_hh2[j * H + u];
     if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g + kPG * tid];
     // per-lane byte offsets (32-bit)
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
-    const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 4u;             // bufA row lr, unit u
-    const unsigned o_y = (unsigned)(lr * kPH + u) * 4u;                 // bufB/C row lr, unit u
+    const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 8u;             // bufA pair (row lr, unit u)
+    const unsigned o_y = (unsigned)(lr * kPH + u) * 8u;                 // bufB/C pair (row lr, unit u)
     const unsigned o_gum = (unsigned)(lrow * a.n_classes + cls) * 4u;   // gumbel row lrow
     const rsrc_t fcr = mk_rsrc(a.fcond);
     const unsigned o_fc = (unsigned)((gate_a ? a.oG2 : a.oF1) + u) * 4u;
@@ -311,7 +337,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
 
     const float4* X0 = reinterpret_cast<const float4*>(lds + L_X0);
     const float4* X1 = reinterpret_cast<const float4*>(lds + L_X1);
-    unsigned* cnt = reinterpret_cast<unsigned*>(lds + L_CNT);  // producer counters per hop
     const int wave = tid >> 6;
     const bool wv_lo = wave < 4;  // waves 0-3: og < 16 (GRU2, hh2, fc2, fc3 <= 16 classes)
     // Per-step operands, issued right after the wave's last publish of the previous step
@@ -367,24 +392,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             tv = bld(mk_rsrc(a.gumbel + ((size_t)tt * a.B + row) * (a.mode == 0 ? a.n_classes : kMolNoise)),
                      (unsigned)(l - 64) * 128u, 0);
     };
-    // publish by the producer waves only: each waits for its own stores, the last one to
-    // arrive (LDS counter) stores the flag
-    auto publish_by = [&](unsigned* flag, unsigned value, unsigned* c, unsigned nprod) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if ((tid & 63) == 0) {
-            const unsigned old = atomicAdd(c, 1u);
-            if (old == nprod - 1) {
-                *c = 0u;
-                __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-    };
-    if (tid < 4) cnt[tid] = 0u;
     if (tid == 0) lds[L_FAIL] = 0.f;
     prefetch(a.t0, a.t0);
     pgum = pgn;
     touch(a.t0 + 1);
     __syncthreads();
+    // gh2 rows computed in stage B by waves 0-3 (r < NRB) and in stage C by waves 4-7
+    constexpr int NRB = NR - NR / 3;
+    const int tl = tid & 255;  // index inside the half that stages
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
         const unsigned seq = (unsigned)t + 1u;
@@ -425,32 +440,38 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2),
                                            gh2[0], gh2[kPNR], gh2[2 * kPNR], h2r);
                     h2r = hn;
-                    bst(p_add(lds[L_X0 + lr * kPH + u], hn), xr, o_u, sA);  // x2 = x1 + h2
-                    bst(hn, xr, o_u, sA + kPH * 4);
-                } else {  // gh1 for GRU1 at the end of this step: published with hop B
-                    bst(p_add(s0, b3[0]), xr, o_u, sA + 2 * kPH * 4);
-                    bst(p_add(s1, b3[1]), xr, o_u, sA + 3 * kPH * 4);
-                    bst(p_add(s2, b3[2]), xr, o_u, sA + 4 * kPH * 4);
+                    bst_tag(p_add(lds[L_X0 + lr * kPH + u], hn), seq, xr, o_u, sA);  // x2 = x1 + h2
+                    bst_tag(hn, seq, xr, o_u, sA + kPH * 8);
+                } else {  // gh1 for GRU1 at the end of this step
+                    const float* b = lds + L_BIAS + (og - 16);  // b_hh1 of unit u
+                    bst_tag(p_add(s0, b[0]), seq, xr, o_u, sA + 2 * kPH * 8);
+                    bst_tag(p_add(s1, b[16]), seq, xr, o_u, sA + 3 * kPH * 8);
+                    bst_tag(p_add(s2, b[32]), seq, xr, o_u, sA + 4 * kPH * 8);
                 }
             }
+            if (!gate_a) {  // gh1 must be in L2 before this wave's y1 (stage B) can be seen
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
-        if (wv_lo) {
-            publish_by(fl + 0 * 64 + w, seq, cnt + 0, 4);
-            __builtin_amdgcn_s_setprio(0);
-        }
+        __builtin_amdgcn_s_setprio(0);
         PSTAMP(1);
-        if (!p_wait(fl + 0 * 64, seq, a.ctl, tid)) return;
-        PSTAMP(2);
-        // ================= stage B: fc1 (waves 4-7) ==========================================
-        if (wv_lo) {
-            for (int i = tid; i < NR * kPK4; i += 256) {
-                const int r = i / kPK4, q = i % kPK4;
-                const unsigned o = (unsigned)(r * 5 * kPH + 4 * q) * 4u;
-                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, o, sA);
-                reinterpret_cast<float4*>(lds + L_X1)[i] = bld4_nt(xr, o, sA + kPH * 4);
+        // ================= stage B: fc1 (waves 4-7, critical) | W_hh2 h2 rows < NRB (0-3) ===
+        if (wv_lo) {  // stage x2 -> X0, h2 -> X1 (polling the tagged pairs)
+#pragma unroll
+            for (int arr = 0; arr < 2; ++arr) {
+                unsigned off[NR];
+                float2* dst[NR];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {  // couple tl of (row m, array arr)
+                    off[m] = (unsigned)((m * 5 + arr) * kPH + 2 * tl) * 8u;
+                    dst[m] = reinterpret_cast<float2*>(lds + (arr ? L_X1 : L_X0) + m * kPH) + tl;
+                }
+                if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
             }
         }
         __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        PSTAMP(2);
         if (!gate_a) {
             __builtin_amdgcn_s_setprio(2);
             float s0 = 0.f;
@@ -471,22 +492,64 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
             if (kc < NR) {
                 const float y = p_add(s0, pc0);
-                bst(y > 0.f ? y : 0.f, xr, o_y, XB_B * 4);
+                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_y, XB_B * 4);
             }
-            publish_by(fl + 1 * 64 + w, seq, cnt + 1, 4);  // also covers gh1 of stage A
             __builtin_amdgcn_s_setprio(0);
             touch(t + 2);
         }
+        // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path: rows r < NRB by
+        // waves 0-3 here, the rest by waves 4-7 in stage C (LDS weights, h2 staged in X1)
+        auto hh2_rows = [&](int r0, int r1, int ul) {
+            const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)ul * 3 * kPK4;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (r < r0 || r >= r1) continue;
+                v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    float4 w4[3];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
+                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) dot4(acc[j], w4[j], x4);
+                }
+                const float t0 = row16_sum(hsum(acc[0]));
+                const float t1 = row16_sum(hsum(acc[1]));
+                const float t2 = row16_sum(hsum(acc[2]));
+                if (kc == r) {
+                    s0 = t0;
+                    s1 = t1;
+                    s2 = t2;
+                }
+            }
+            if (kc >= r0 && kc < r1) {
+                float* gh2 = lds + L_GH2 + ul * 3 * kPNR + kc;
+                const float* b = lds + L_BIAS + 48 + ul;  // b_hh2 of unit 16 w + ul
+                gh2[0] = p_add(s0, b[0]);
+                gh2[kPNR] = p_add(s1, b[16]);
+                gh2[2 * kPNR] = p_add(s2, b[32]);
+            }
+        };
+        if (gate_a) hh2_rows(0, NRB, og);
         PSTAMP(3);
-        if (!p_wait(fl + 1 * 64, seq, a.ctl, tid)) return;
-        PSTAMP(4);
-        // ================= stage C: fc2 (waves 0-3, critical) | W_hh2 h2 (waves 4-7) ========
-        if (wv_lo) {
-            for (int i = tid; i < NR * kPK4; i += 256)
-                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_B * 4);
+        // ================= stage C: fc2 (waves 0-3, critical) | W_hh2 h2 rows >= NRB (4-7) ===
+        if (!wv_lo) {  // stage y1 -> X0
+            unsigned off[NR];
+            float2* dst[NR];
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                off[m] = (unsigned)(m * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
+            }
+            if (!poll_couples<NR>(xr, off, XB_B * 4, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
-        if (wv_lo) {
+        if (lds[L_FAIL] != 0.f) return;
+        PSTAMP(4);
+        if (gate_a) {
             __builtin_amdgcn_s_setprio(2);
             float s0 = 0.f;
 #pragma unroll
@@ -506,69 +569,27 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
             if (kc < NR) {
                 const float y = p_add(s0, pf2);
-                bst(y > 0.f ? y : 0.f, xr, o_y, XB_C * 4);
+                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_y, XB_C * 4);
             }
-            publish_by(fl + 2 * 64 + w, seq, cnt + 2, 4);
             __builtin_amdgcn_s_setprio(0);
         } else {
-            // off the critical path: gh2 = W_hh2 h2 + b_hh2 for the next step's GRU2
-            v2f acc[3][NR];
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-#pragma unroll
-                for (int r = 0; r < NR; ++r) acc[j][r] = (v2f){0.f, 0.f};
-            const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)(og - 16) * 3 * kPK4;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                __builtin_amdgcn_sched_barrier(0);
-                float4 w4[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) dot4(acc[j][r], w4[j], x4);
-                }
-            }
-            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const float t0 = row16_sum(hsum(acc[0][r]));
-                const float t1 = row16_sum(hsum(acc[1][r]));
-                const float t2 = row16_sum(hsum(acc[2][r]));
-                if (kc == r) {
-                    s0 = t0;
-                    s1 = t1;
-                    s2 = t2;
-                }
-            }
-            if (kc < NR) {  // gh2 for the next step's GRU2
-                float* gh2 = lds + L_GH2 + (og - 16) * 3 * kPNR + kc;
-                gh2[0] = p_add(s0, bh2[0]);
-                gh2[kPNR] = p_add(s1, bh2[1]);
-                gh2[2 * kPNR] = p_add(s2, bh2[2]);
-            }
+            hh2_rows(NRB, NR, og - 16);
         }
         PSTAMP(5);
-        if (!p_wait(fl + 2 * 64, seq, a.ctl, tid)) return;
-        PSTAMP(6);
-        // ================= stage D: fc3 -> per-slot candidates (wave 0 publishes) ===========
-        // GRU1 operands (gh1 published with hop B; P1 / cI L2-warm) and the next step's
-        // epilogue operands: waves 1-7 now, wave 0 after it publishes hop D
-        float pG[NR][3];
-        auto load_gh1 = [&]() {
+        // ================= stage D: fc3 -> per-slot candidates ==============================
+        if (wv_lo) {  // stage y2 -> X0
+            unsigned off[NR];
+            float2* dst[NR];
 #pragma unroll
-            for (int r = 0; r < NR; ++r)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    pG[r][j] = bld_nt(xr, o_tid, sA + (unsigned)(r * 5 * kPH + (2 + j) * kPH) * 4u);
-        };
-        if (wv_lo) {
-            for (int i = tid; i < NR * kPK4; i += 256)
-                reinterpret_cast<float4*>(lds + L_X0)[i] = bld4_nt(xr, (unsigned)i * 16u, XB_C * 4);
+            for (int m = 0; m < NR; ++m) {
+                off[m] = (unsigned)(m * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
+            }
+            if (!poll_couples<NR>(xr, off, XB_C * 4, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        PSTAMP(6);
         {
             float s0 = 0.f;
             if (has_cls) {
@@ -606,6 +627,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
             }
             __syncthreads();
+            PSTAMP(11);
             if (wave == 0) {
                 if (a.mode == 0) {
                     // slot candidate per row, tagged with the step (no flag, no wait)
@@ -647,7 +669,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 }
             }
         }
-        load_gh1();
+        // GRU1 operands: gh1 of this step (tagged, from stage A), P1 / cI (L2-warm), and the
+        // next step's epilogue operands
+        // gh1 (stage A) was drained by its producer waves before they stored y1 (stage B),
+        // and this workgroup has seen every slot's y1 tag (stage C staging): plain loads
+        float pG[NR][3];
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                pG[r][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    xr, o_tid * 2u, sA + (unsigned)((r * 5 + 2 + j) * kPH) * 8u, kCpNT));
         prefetch(t, t + 1);
         pgum = pgn;
         PSTAMP(7);

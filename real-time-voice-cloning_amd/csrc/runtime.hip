@@ -1205,10 +1205,10 @@ void persist_phase_report(wrnn_handle* h, int t) {
     std::vector<uint32_t> ph((size_t)kPG * kPM * kPPhases);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return;
     if (hipMemcpy(ph.data(), h->pws.phases.p, ph.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
-    static const char* names[] = {"start", "A", "hopA", "B", "hopB", "C", "hopC", "D", "hopD", "sample", "gru1"};
+    static const char* names[] = {"start", "A", "hopA", "B", "hopB", "C", "hopC", "D", "hopD", "sample", "gru1", "fc3"};
     std::fprintf(stderr, "[wrnn persist phases] step %d: last workgroup of each group, us from the group's first start"
                          " (wave 0 | wave 4)\n", t);
-    for (int i = 0; i < 11; ++i) {
+    for (int i = 0; i < 12; ++i) {
         double med[2] = {0, 0}, mxx[2] = {0, 0};
         for (int wv = 0; wv < 2; ++wv) {
             std::vector<double> d;
