@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // (waves 0-3: hop C, waves 4-7: hop B) so the publish never waits on them:
     //   pP/pC  P1(tg+1), cI(tg+1) of this thread's GRU1 unit   (end of step tg)
     //   pc*    per-frame conditioning of step te's epilogues  (stages A-C of step te)
-    //   pgn    Gumbel noise of step te, class cls            (stage D of step te)
+    //   pgn    Gumbel noise of step te, class cls (copied to pgum at the end of step te-1)
     float pP[NR][3], pC[NR];
     float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f, pgn = 0.f;
     auto prefetch = [&](int tg, int te) {
@@ -590,6 +590,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(6);
+        float pG[NR][3];  // GRU1 operands, loaded once this wave's fc3 work is issued
+        auto gru1_loads = [&]() {
+            // gh1 (stage A) was drained by its producer waves before they stored y1 (stage B),
+            // and this workgroup has seen every slot's y1 tag (stage C staging): plain loads
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    pG[r][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        xr, o_tid * 2u, sA + (unsigned)((r * 5 + 2 + j) * kPH) * 8u, kCpNT));
+            prefetch(t, t + 1);  // pgn, not pgum: the fc3 epilogue still reads pgum
+        };
+
         {
             float s0 = 0.f;
             if (has_cls) {
@@ -613,6 +626,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     if (kc == r) s0 = t0;
                 }
             }
+            if (!FC3R) gru1_loads();  // (10-bit: after the argmax, register budget)
             float* red = lds + L_RED;  // [og][r][value, class]
             if (kc < NR) {
                 float val = -INFINITY;
@@ -669,19 +683,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 }
             }
         }
-        // GRU1 operands: gh1 of this step (tagged, from stage A), P1 / cI (L2-warm), and the
-        // next step's epilogue operands
-        // gh1 (stage A) was drained by its producer waves before they stored y1 (stage B),
-        // and this workgroup has seen every slot's y1 tag (stage C staging): plain loads
-        float pG[NR][3];
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                pG[r][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    xr, o_tid * 2u, sA + (unsigned)((r * 5 + 2 + j) * kPH) * 8u, kCpNT));
-        prefetch(t, t + 1);
-        pgum = pgn;
+        if (FC3R) gru1_loads();
         PSTAMP(7);
         if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
         PSTAMP(8);
@@ -773,6 +775,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X1 + r * kPH + tid] = hn;
         }
         asm volatile("" ::"v"(tv));  // the L2 warm-up load retires here at the latest
+        pgum = pgn;
         __syncthreads();
         PSTAMP(10);
     }
