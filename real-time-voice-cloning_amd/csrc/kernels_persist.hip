@@ -56,7 +56,19 @@ __device__ __forceinline__ float row16_sum(float v) {
     return v;
 }
 
-__device__ __forceinline__ float p_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate nonlinearities on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each):
+// sigmoid(x) = 1 / (1 + 2^(-x log2 e)), tanh(x) = 1 - 2 / (2^(2x log2 e) + 1). Within a few ulp
+// of torch's vectorised sigmoid / tanh -- the same order as the fp32 summation-order
+// differences of the matrix products -- at a fraction of the cost of expf / IEEE division /
+// tanhf; the RAW label parity tests run on this path.
+__device__ __forceinline__ float p_sigmoid(float x) {
+    const float e = __builtin_amdgcn_exp2f(-x * 1.4426950408889634f);
+    return __builtin_amdgcn_rcpf(1.0f + e);
+}
+__device__ __forceinline__ float p_tanh(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
 // torch GRUCell gate arithmetic (same operation order as kernels_step.hip gru_cell)
 __device__ __forceinline__ float p_gru(float gi_r, float gi_z, float gi_n, float gh_r, float gh_z,
                                        float gh_n, float h) {
@@ -64,7 +76,7 @@ __device__ __forceinline__ float p_gru(float gi_r, float gi_z, float gi_n, float
     const float r = p_sigmoid(gh_r + gi_r);
     const float z = p_sigmoid(gh_z + gi_z);
     const float ghr = gh_n * r;
-    const float n = tanhf(gi_n + ghr);
+    const float n = p_tanh(gi_n + ghr);
     const float d = h - n;
     const float dz = d * z;
     return dz + n;
