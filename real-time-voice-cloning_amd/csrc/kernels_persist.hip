@@ -229,17 +229,23 @@ __device__ __forceinline__ void bst_tag(float v, unsigned tag, rsrc_t r, unsigne
 template <int M>
 __device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M], unsigned so,
                                              unsigned want, float2* const (&dst)[M], unsigned* ctl) {
+    // spin on the first couple only (a thread's couples all come from one producer slot), then
+    // take the whole set and verify every tag; keeps the polling traffic in L2 small
     const unsigned t0 = p_now();
     unsigned n = 0;
     while (true) {
-        bool ok = true;
+        const u4v c0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off[0], so, kCpNT);
+        if (__all(c0.y == want && c0.w == want)) {
+            bool ok = true;
+            *dst[0] = make_float2(__uint_as_float(c0.x), __uint_as_float(c0.z));
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off[m], so, kCpNT);
-            *dst[m] = make_float2(__uint_as_float(c.x), __uint_as_float(c.z));
-            ok = ok && c.y == want && c.w == want;
+            for (int m = 1; m < M; ++m) {
+                const u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off[m], so, kCpNT);
+                *dst[m] = make_float2(__uint_as_float(c.x), __uint_as_float(c.z));
+                ok = ok && c.y == want && c.w == want;
+            }
+            if (__all(ok)) return true;
         }
-        if (__all(ok)) return true;
         if ((++n & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
             if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
             return false;
@@ -468,18 +474,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         __builtin_amdgcn_s_setprio(0);
         PSTAMP(1);
         // ================= stage B: fc1 (waves 4-7, critical) | W_hh2 h2 rows < NRB (0-3) ===
-        if (wv_lo) {  // stage x2 -> X0, h2 -> X1 (polling the tagged pairs)
+        if (wv_lo) {  // stage x2 -> X0, h2 -> X1 (polling the tagged pairs, one pass)
+            unsigned off[2 * NR];
+            float2* dst[2 * NR];
 #pragma unroll
-            for (int arr = 0; arr < 2; ++arr) {
-                unsigned off[NR];
-                float2* dst[NR];
-#pragma unroll
-                for (int m = 0; m < NR; ++m) {  // couple tl of (row m, array arr)
-                    off[m] = (unsigned)((m * 5 + arr) * kPH + 2 * tl) * 8u;
-                    dst[m] = reinterpret_cast<float2*>(lds + (arr ? L_X1 : L_X0) + m * kPH) + tl;
-                }
-                if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+            for (int m = 0; m < 2 * NR; ++m) {  // couple tl of (row m / 2, array m % 2)
+                off[m] = (unsigned)(((m >> 1) * 5 + (m & 1)) * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + ((m & 1) ? L_X1 : L_X0) + (m >> 1) * kPH) + tl;
             }
+            if (!poll_couples<2 * NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
