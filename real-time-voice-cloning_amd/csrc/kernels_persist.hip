@@ -3,7 +3,8 @@
 // Reference step body: vocoder/models/fatchord_version.py:192-236. One launch runs a chunk of
 // steps for all fold rows. The 256 workgroups (one per CU, 512 threads) form 8 groups from the
 // workgroups that report the same HW_REG_XCC_ID, so every group lives on one XCD and shares
-// its L2. Group g owns fold rows g, g+8, ... (NR rows; the host pads the row count to 8*NR)
+// its L2. Group g owns fold rows rb+g, rb+g+8, ... (NR rows of one row batch; the host pads
+// the row count to a multiple of 8*NR and launches once per batch)
 // and holds ALL step weights, spread over its 32 workgroups (slot w owns GRU units / outputs
 // [16w, 16w+16) and fc3 classes [cpw*w, cpw*(w+1))): registers hold W_ih2[:, :512] and W_hh1
 // (r,z,n rows of the slot's units) and the fc1/fc2 rows; LDS holds the W_hh2 rows and the fc3
@@ -287,6 +288,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     __syncthreads();
     if (!s_ok) return;
     const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int g0 = a.rb + g;  // first fold row of this group in this launch (row batch)
     const int w = __builtin_amdgcn_readfirstlane(s_slot);
     const int og = tid >> 4, kc = tid & 15;
     constexpr int H = kPH;
@@ -324,10 +326,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     float h1[NR], h2r = 0.f;
     const bool own = gate_a && kc < NR;
     const int lr = kc < NR ? kc : 0;
-    const int lrow = g + kPG * lr;  // row of this lane's epilogue
+    const int lrow = g0 + kPG * lr;  // row of this lane's epilogue
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        const int row = g + kPG * r;
+        const int row = g0 + kPG * r;
         h1[r] = a.st_h1[(size_t)row * H + tid];
         lds[L_X0 + r * kPH + tid] = a.st_x1[(size_t)row * H + tid];
         lds[L_X1 + r * kPH + tid] = h1[r];
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid], w0j = a.w0[tid];
     if (tid < 96) lds[L_BIAS + tid] = (tid < 48 ? a.b_hh1 : a.b_hh2)[(tid % 48 / 16) * H + 16 * w + (tid & 15)];
     const float bcls = has_cls ? a.b_fc3[cls] : 0.f;
-    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g + kPG * tid];
+    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
     // per-lane byte offsets (32-bit)
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
     const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 8u;             // bufA pair (row lr, unit u)
@@ -368,8 +370,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) pP[r][0] = pP[r][1] = pP[r][2] = pC[r] = 0.f;
         if (tg + 1 < a.S) {
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(tg + 1) * a.B + g) * 3 * H);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(tg + 1) * a.B + g) * H);
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(tg + 1) * a.B + g0) * 3 * H);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(tg + 1) * a.B + g0) * H);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
 #pragma unroll
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         const int i = tid - 256;
         const int li = w + kPM * i;
         if (tt >= a.S || i < 0 || li >= NR * lines_r) return;
-        const int r = li / lines_r, l = li % lines_r, row = g + kPG * r;
+        const int r = li / lines_r, l = li % lines_r, row = g0 + kPG * r;
         if (l < 48)
             tv = bld(mk_rsrc(a.P1 + ((size_t)tt * a.B + row) * 3 * H), (unsigned)l * 128u, 0);
         else if (l < 64)
@@ -733,7 +735,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     }
                     lds[L_SX + r] = xv;
                     if (w == 0) {
-                        const unsigned ro = (unsigned)((g + kPG * r) * a.ld);
+                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
                                                               ro * 2u, (unsigned)t * 2u, 0);
                         bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -743,7 +745,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         } else if (tid < NR) {
             // MOL: vocoder/distribution.py:104-140; the Philox draws were turned into
             // gm_k = log(-log(u1_k)) and lu = log(u2) - log(1 - u2) by k_mol_noise
-            const int r = tid, row = g + kPG * r;
+            const int r = tid, row = g0 + kPG * r;
             const unsigned lo = (unsigned)(r * 64) * 4u;
             const unsigned so = (XB_D + XB_D_LOG) * 4;
             const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
@@ -801,7 +803,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         if (w == 0)
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                const int row = g + kPG * r;
+                const int row = g0 + kPG * r;
                 a.st_x1[(size_t)row * H + tid] = lds[L_X0 + r * kPH + tid];
                 a.st_h1[(size_t)row * H + tid] = lds[L_X1 + r * kPH + tid];
             }
@@ -942,7 +944,7 @@ int persist_variant_ok(int nr, int cpw) {
 }
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
-    if (a.B != kPG * a.nr || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)
+    if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)
         return hipErrorInvalidValue;
     const bool r = a.cpw > 16;
     switch (a.nr) {

@@ -183,6 +183,7 @@ struct wrnn_handle {
     int last_engine = WRNN_ENGINE_CHAIN;
     bool persist_failed = false;    // a persistent launch failed on this device: stay on CHAIN
     int last_Bp = 0;                // rows the last call ran (padded to 8 * rows-per-group)
+    int p_nr = 0, p_nbatch = 0;     // PERSIST: rows per group per launch, row batches
     std::vector<hipEvent_t> pev;    // PERSIST timing events (start, end) per launch
     std::vector<int> pev_steps;
     double p_step_bytes = 0, p_step_flops = 0;  // algorithmic per step
@@ -1185,6 +1186,7 @@ int run_chain(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     return WRNN_OK;
 }
 
+constexpr double kPersistWsBytes = 96.0 * (1 << 30);  // P1 + cI + noise cap (of 288 GB HBM)
 constexpr int kPersistFallback = 1;  // internal: retry the call on the CHAIN engine
 
 bool persist_device_ok(wrnn_handle* h) {
@@ -1301,24 +1303,43 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.phases = (uint32_t*)P.phases.p;
     }
     HIPC(launch_persist_init(a, st));
-    HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
-    HIPC(hipMemsetAsync(P.xbuf.p, 0, persist_xbuf_floats() * sizeof(float), st));  // step tags
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
+    // launches: row batches in order, each in time chunks (1000 steps when a progress callback
+    // wants reports, else one chunk); the step tags restart with every batch, so the exchange
+    // area and flags are cleared before each batch's first chunk
+    const int nb = h->p_nbatch;
+    a.nr = h->p_nr;
     const int G = cb ? 1000 : S;
     const int nchunks = (S + G - 1) / G;
+    const int nl = nb * nchunks;
     for (auto e : h->pev) (void)hipEventDestroy(e);
     h->pev.clear();
     h->pev_steps.clear();
-    if (h->timing) CHECK(P.stamps.alloc((size_t)nchunks * 2 * sizeof(uint32_t)));
+    if (h->timing) CHECK(P.stamps.alloc((size_t)nl * 2 * sizeof(uint32_t)));
     const auto t_start = std::chrono::steady_clock::now();
-    std::vector<hipEvent_t> done(nchunks, nullptr);
+    std::vector<hipEvent_t> done(nl, nullptr);
+    // progress in reference units: step i of S, scaled over the batches
+    auto report = [&](int l) -> int {
+        (void)hipEventSynchronize(done[l]);
+        const int b = l / nchunks, i = ((l % nchunks) * G + (long long)b * S) / nb;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        if (cb(user, i, S, B, ((long long)b * S + (l % nchunks) * G + 1) / std::max(el, 1e-9) * (B / nb) / 1000.0))
+            return fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+        return WRNN_OK;
+    };
     int rc = WRNN_OK;
-    for (int c = 0; c < nchunks && rc == WRNN_OK; ++c) {
+    for (int l = 0; l < nl && rc == WRNN_OK; ++l) {
+        const int b = l / nchunks, c = l % nchunks;
+        a.rb = b * kPG * a.nr;
         a.t0 = c * G;
         a.t1 = std::min(S, a.t0 + G);
-        // registration words only: an error code from an earlier chunk stays visible
+        if (c == 0) {
+            HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
+            HIPC(hipMemsetAsync(P.xbuf.p, 0, persist_xbuf_floats() * sizeof(float), st));  // step tags
+        }
+        // registration words only: an error code from an earlier launch stays visible
         HIPC(hipMemsetAsync(P.ctl.p, 0, PC_ERR * sizeof(unsigned), st));
-        a.stamps = h->timing ? (uint32_t*)P.stamps.p + 2 * c : nullptr;
+        a.stamps = h->timing ? (uint32_t*)P.stamps.p + 2 * l : nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->timing) {
             HIPC(hipEventCreate(&e0));
@@ -1331,27 +1352,15 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(launch_persist(a, st));
         if (h->timing) HIPC(hipEventRecord(e1, st));
         if (cb) {
-            if (hipEventCreateWithFlags(&done[c], hipEventDisableTiming) != hipSuccess ||
-                hipEventRecord(done[c], st) != hipSuccess) {
+            if (hipEventCreateWithFlags(&done[l], hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(done[l], st) != hipSuccess) {
                 rc = fail(WRNN_ERR_HIP, "event record");
                 break;
             }
-            if (c >= 1) {  // report the previous chunk (one chunk stays queued ahead)
-                (void)hipEventSynchronize(done[c - 1]);
-                const int i = a.t0 - G;
-                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-                if (cb(user, i, S, B, (i + 1) / std::max(el, 1e-9) * B / 1000.0))
-                    rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
-            }
+            if (l >= 1) rc = report(l - 1);  // one launch stays queued ahead
         }
     }
-    if (rc == WRNN_OK && cb) {
-        (void)hipEventSynchronize(done[nchunks - 1]);
-        const int i = (nchunks - 1) * G;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-        if (cb(user, i, S, B, (i + 1) / std::max(el, 1e-9) * B / 1000.0))
-            rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
-    }
+    if (rc == WRNN_OK && cb) rc = report(nl - 1);
     for (auto e : done)
         if (e) (void)hipEventDestroy(e);
     if (rc) return rc;
@@ -1373,12 +1382,14 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
                           "rnn2.bias_hh_l0", "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias",
                           "fc3.weight", "fc3.bias"})
         wparams += (double)h->host[k].size();
-    h->p_step_bytes = 4.0 * wparams + B * ((h->feat + h->R) * 4.0 + 2.0);
+    // per launch: one row batch (real rows averaged over the batches)
+    const double rows_l = (double)B / nb;
+    h->p_step_bytes = 4.0 * wparams + rows_l * ((h->feat + h->R) * 4.0 + 2.0);
     double macs = 0;
     for (const char* k : {"I.weight", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn2.weight_ih_l0",
                           "rnn2.weight_hh_l0", "fc1.weight", "fc2.weight", "fc3.weight"})
         macs += (double)h->host[k].size();
-    h->p_step_flops = 2.0 * macs * B;
+    h->p_step_flops = 2.0 * macs * rows_l;
     return WRNN_OK;
 }
 
@@ -1424,12 +1435,22 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         else if (!std::strcmp(env, "auto")) want = WRNN_ENGINE_AUTO;
     }
     std::string why;
-    const int nr = (B + kPG - 1) / kPG;
+    // PERSIST row batches: the largest register-resident rows-per-group variant bounds one
+    // launch at 8 * nr_max rows; more rows run as consecutive launches over row batches, with
+    // the rows spread evenly over the batches (nr rows per group each)
+    int nr_max = 0;
+    if (h->pw.ok)
+        for (int r = kPNR; r >= 1 && !nr_max; --r)
+            if (persist_variant_ok(r, h->pw.cpw)) nr_max = r;
+    const int nbatch = nr_max ? (B + kPG * nr_max - 1) / (kPG * nr_max) : 0;
+    const int nr = nbatch ? (B + kPG * nbatch - 1) / (kPG * nbatch) : 0;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
         if (!h->pw.ok) why = "model is not fatchord with rnn_dims = fc_dims = 512 and <= 1024 classes";
-        else if (B > kPG * kPNR) why = std::to_string(B) + " fold rows > " + std::to_string(kPG * kPNR);
-        else if (!persist_variant_ok(nr, h->pw.cpw)) why = "no register-resident variant for this row count";
+        else if (!nr_max) why = "no register-resident variant for this class count";
+        else if ((double)S * kPG * nr * nbatch * (4 * kPH + h->n_classes) * 4.0 > kPersistWsBytes)
+            why = "P1 / noise workspace for " + std::to_string(B) + " rows x " + std::to_string(S) +
+                  " steps exceeds " + std::to_string((long long)(kPersistWsBytes / (1 << 30))) + " GiB";
         else if (h->persist_failed) why = "a persistent launch failed earlier on this handle";
         else if (S >= (1 << 21)) why = "seq_len >= 2^21 (step tags)";
         else if (!persist_device_ok(h)) why = "device is not a 256-CU gfx950";
@@ -1437,7 +1458,9 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         if (want == WRNN_ENGINE_PERSIST && !use_p)
             return fail(WRNN_ERR_INVALID, "persist engine unavailable: " + why);
     }
-    const int Bp = use_p ? kPG * nr : B;  // persistent groups carry nr rows each
+    const int Bp = use_p ? kPG * nr * nbatch : B;  // persistent groups carry nr rows per batch
+    h->p_nr = use_p ? nr : 0;
+    h->p_nbatch = use_p ? nbatch : 0;
     CHECK(ensure_workspace(h, Bp, S, P, Fr, Tmax));
     auto& ws = h->ws;
     h->last_B = B;

@@ -144,8 +144,9 @@ hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipSt
 
 // ---------------------------------------------------------------------------------------
 // Persistent, weight-stationary fatchord recurrence (kernels_persist.hip). 8 XCD-local groups
-// of 32 workgroups; group g owns fold rows g, g+8, ... g+8(NR-1) (the host pads the row count
-// to 8*NR so every group carries the same number of rows).
+// of 32 workgroups; in one launch group g owns fold rows rb+g, rb+g+8, ... rb+g+8(NR-1): the
+// host pads the row count to a multiple of 8*NR and runs one launch per row batch when the
+// rows exceed what one launch holds register-resident.
 // ---------------------------------------------------------------------------------------
 constexpr int kPG = 8;       // groups (one per XCD)
 constexpr int kPM = 32;      // workgroups per group
@@ -171,7 +172,8 @@ struct PersistArgs {
     unsigned* flags;        // [kPG][4 hops][64]; monotonic step counters within one call
     float* xbuf;            // per-group exchange area (persist_xbuf_floats())
     int t0, t1, S;          // steps [t0, t1) of S
-    int B, nr;              // padded rows (= 8 * nr)
+    int B, nr, rb;          // B: row stride of every [t][row] array (padded rows);
+                            // this launch runs rows rb + g + 8 r, r < nr (one row batch)
     int mode, n_classes, hop, cpw;  // cpw = classes per workgroup
     const RowInfo* rows;    // [B]
     const float4* wreg;     // [kPM][kPT][persist_reg_f4(cpw)]

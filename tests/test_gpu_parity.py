@@ -117,10 +117,12 @@ def test_upsample_network_matches_oracle():
     np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize('n_utts', [3, 4, 6])
+@pytest.mark.parametrize('n_utts', [3, 4, 6, 10])
 def test_persist_multi_row_groups_match_oracle(n_utts):
-    """5 fold rows per utterance -> 15 / 20 / 30 rows: 2, 3 and 4 rows per XCD group (the
-    padded-row variants of the persistent engine), every row against the oracle."""
+    """5 fold rows per utterance -> 15 / 20 / 30 / 50 rows: 2 and 3 rows per XCD group (the
+    padded-row variants of the persistent engine) and, past 24 rows, consecutive launches over
+    row batches (30 rows -> 2 batches of 2 rows per group, 50 -> 3 batches of 3), every row
+    against the oracle."""
     import torch
     from oracle.wavernn_oracle import oracle_infer_waveform
     from wavernn_amd.hparams import sp
@@ -144,3 +146,28 @@ def test_persist_multi_row_groups_match_oracle(n_utts):
         got = lab[row_off[u]:row_off[u + 1]]
         assert np.array_equal(got, ref['labels']), \
             f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'
+
+
+def test_persist_row_batches_mol_within_tolerance():
+    """MOL float path over two row batches (6 utterances x 5 rows = 30 rows)."""
+    import torch
+    from oracle.wavernn_oracle import oracle_infer_waveform
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_mol_tiny')
+    m, hp, sd = make_model(meta)
+    n_utts = 6
+    mels = [synth_mel(meta['n_frames'], 200 + u) / sp.max_abs_value for u in range(n_utts)]
+    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
+    m.set_engine('persist')
+    m.set_seed(meta['noise_seed'])
+    out, row_off, S = m.generate_batch_device(dev, True, meta['target'], meta['overlap'])
+    assert m.last_engine() == 'persist'
+    out = out.cpu().numpy()
+    for u in range(n_utts):
+        ref = oracle_infer_waveform(sd, hp, meta['model_type'], mels[u] * sp.max_abs_value,
+                                    target=meta['target'], overlap=meta['overlap'],
+                                    seed=meta['noise_seed'], stream=u)
+        got = out[row_off[u]:row_off[u + 1]].astype(np.float64)
+        rms = float(np.sqrt(np.mean((got - ref['samples']) ** 2)))
+        assert rms <= MOL_RMS_TOL, f'utt {u}: per-fold sample RMS {rms}'
