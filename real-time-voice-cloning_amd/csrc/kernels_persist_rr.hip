@@ -1,0 +1,727 @@
+// Persistent, weight-stationary recurrence of the runtimeracer WaveRNN (PERSIST engine, second
+// topology).
+//
+// Reference step body: vocoder/models/runtimeracer_version.py:244-270 (rnn_dims = fc_dims = 256):
+//   x1 = I(x0) + h1'            h1' = rnn1(I(x0), h1)
+//   x2 = x1 + rnn2(x1, h2)      x3 = x2 + rnn3([x2, a2], h3)      x4 = x3 + rnn4(x3, h4)
+//   y1 = fc1([x4, a3])          y2 = relu(fc2(y1))
+//   y3 = fc3([y2, a4])          y4 = relu(fc4(y3))                 logits = fc5(y4)
+//
+// Same execution model as kernels_persist.hip: 8 groups of 32 workgroups (one group per XCD,
+// formed from HW_REG_XCC_ID), 512 threads per workgroup, every weight of the step resident in
+// registers for the whole launch, and in-group exchanges of tagged (value, step) pairs through
+// the XCD's shared L2. Slot w owns units / outputs [8w, 8w + 8) of every layer and fc5 classes
+// [cpw w, cpw (w + 1)). The 512 threads form four quads of 128 (og = unit 0..7, kc = k-chunk
+// 0..15); each quad holds a different set of weight rows (host layout: pack_persist_rr):
+//   quad 0: W_ih2 | W_ih3[:, :256] | fc4      quad 1: W_ih4 | W_hh1 | fc3[:, :256]
+//   quad 2: W_hh2 | W_hh3 | fc2               quad 3: W_hh4 | fc1[:, :256]
+// and in LDS the slot's fc5 rows [32 classes][256] (staged to registers only during stage 8).
+// Per step eight hops lie on the dependency chain (GRU2, GRU3, GRU4, fc1, fc2, fc3, fc4, fc5
+// candidates) and the recurrent products W_hh h run in the idle quads of earlier stages:
+//   stage 1  q0 GRU2 -> (x2, h2)     q1 gh1 = W_hh1 h1 (published)   q3 gh4 = W_hh4 h4 (local)
+//   stage 2  q0 GRU3 -> (x3, h3)     q2 gh2 = W_hh2 h2 (next step)
+//   stage 3  q1 GRU4 -> (x4, h4)     q2 gh3 = W_hh3 h3 (next step)
+//   stage 4  q3 fc1 -> y1            stage 5  q2 fc2 -> y2
+//   stage 6  q1 fc3 -> y3            stage 7  q0 fc4 -> y4
+//   stage 8  all quads fc5 -> per-slot Gumbel-max candidates (RAW) / logits (MOL)
+// then, redundantly in every workgroup, the sample and GRU1 of the next step for all 256 units
+// (gi = P1 + v x with P1 = W_ih1 (I c) + b precomputed, the rank-1 x term of kernels_persist.hip).
+// Every inter-stage LDS buffer is written only by a poll that follows a barrier after its
+// last reader (ping-pong XA / XB for the chain, one buffer per h_k), so no poll races a reader.
+#include "wrnn_kernels.h"
+#include "persist_common.h"
+
+namespace wrnn {
+
+namespace {
+
+constexpr int RH = kRH;
+constexpr int RK4 = RH / 4;    // float4 per row
+constexpr int RU = RH / kPM;   // units per slot (8)
+static_assert(RU == 8, "quad layout assumes 8 units per slot");
+
+// exchange area per group (floats)
+constexpr int RX_G = 0;                                    // GRU hops [3][kRNR][2][RH] pairs
+constexpr int RX_G_SZ = kRNR * 2 * RH * 2;
+constexpr int RX_F = RX_G + 3 * RX_G_SZ;                   // fc hops [4][kRNR][RH] pairs
+constexpr int RX_F_SZ = kRNR * RH * 2;
+constexpr int RX_GH1 = RX_F + 4 * RX_F_SZ;                 // gh1 [2 parity][kRNR][3 RH] floats
+constexpr int RX_GH1_SZ = kRNR * 3 * RH;
+constexpr int RX_D = RX_GH1 + 2 * RX_GH1_SZ;               // candidates [kPM][kRNR] pairs
+constexpr int RX_D_LOG = kPM * kRNR * 2;
+constexpr int RX_GROUP = RX_D + RX_D_LOG + kRNR * 32 + 64; // + MOL logits [kRNR][32]
+
+// LDS carve (floats)
+constexpr int L_XA = 0;                          // [kRNR][RH] stage inputs, ping
+constexpr int L_XB = L_XA + kRNR * RH;           // pong
+constexpr int L_H1 = L_XB + kRNR * RH;           // h1 (W_hh1 input), h2, h3, h4
+constexpr int L_H2 = L_H1 + kRNR * RH;
+constexpr int L_H3 = L_H2 + kRNR * RH;
+constexpr int L_H4 = L_H3 + kRNR * RH;
+constexpr int L_GH2 = L_H4 + kRNR * RH;          // [3][RU][kRNR] gh2 = W_hh2 h2 + b (slot units)
+constexpr int L_GH3 = L_GH2 + 3 * RU * kRNR;
+constexpr int L_GH4 = L_GH3 + 3 * RU * kRNR;
+constexpr int L_RED = L_GH4 + 3 * RU * kRNR;     // [32 classes][kRNR][value, class]
+constexpr int L_SX = L_RED + 32 * kRNR * 2;      // sampled x per row
+constexpr int L_FAIL = L_SX + 8;
+constexpr int L_DUMMY = L_SX + 12;               // sink of padding poll lanes (float2)
+constexpr int L_RI = L_SX + 16;                  // RowInfo of the group's rows
+constexpr int L_CB = L_RI + 6 * kRNR + 4;        // slot constants, see CB_*
+constexpr int CB_IH2 = 0, CB_IH4 = 24, CB_HH1 = 48, CB_HH2 = 72, CB_HH3 = 96, CB_HH4 = 120,
+              CB_F2 = 144, CB_F4 = 152;
+constexpr int L_W5 = L_CB + 160;                 // fc5 rows of the slot [32][RH]
+constexpr int L_TOTAL = L_W5 + 32 * RH;
+static_assert(L_DUMMY % 2 == 0, "float2 sink");
+static_assert(L_W5 % 4 == 0, "float4 weights");
+
+// per-row dot products of register-resident gate rows (3 gates of unit og, k-chunk kc) with the
+// NR staged rows of X; lane kc == r of each 16-lane row keeps row r's sums
+template <int NR, int B0>
+__device__ __forceinline__ void mv3(const float4 (&wr)[kRNW], const float4* X, int kc, float& s0,
+                                    float& s1, float& s2) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
+        float4 xq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xq[i] = X[r * RK4 + 16 * i + kc];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) dot4(acc[j], wr[B0 + 4 * j + i], xq[i]);
+        const float t0 = row16_sum(hsum(acc[0]));
+        const float t1 = row16_sum(hsum(acc[1]));
+        const float t2 = row16_sum(hsum(acc[2]));
+        if (kc == r) {
+            s0 = t0;
+            s1 = t1;
+            s2 = t2;
+        }
+    }
+}
+template <int NR, int B0>
+__device__ __forceinline__ float mv1(const float4 (&wr)[kRNW], const float4* X, int kc) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        v2f acc = {0.f, 0.f};
+        float4 xq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xq[i] = X[r * RK4 + 16 * i + kc];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dot4(acc, wr[B0 + i], xq[i]);
+        const float t = row16_sum(hsum(acc));
+        if (kc == r) s = t;
+    }
+    return s;
+}
+
+// Poll one hop of NA arrays x NR rows x RH tagged pairs into LDS (dst0 / dst1 [kRNR][RH]);
+// every thread takes couples tid, tid + 512, ...; padding lanes re-poll a valid couple into a
+// sink. False on abort / timeout.
+template <int NR, int NA>
+__device__ __forceinline__ bool poll_hop(rsrc_t xr, unsigned so, unsigned seq, float* dst0,
+                                         float* dst1, float* sink, unsigned* ctl, int tid) {
+    constexpr int TOT = NR * NA * (RH / 2);
+    constexpr int M = (TOT + kPT - 1) / kPT;
+    unsigned off[M];
+    float2* dst[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int c = tid + kPT * m;
+        const bool valid = c < TOT;
+        const int cc = valid ? c : c % TOT;
+        const int r = cc / (NA * (RH / 2)), a = (cc / (RH / 2)) % NA, cp = cc % (RH / 2);
+        off[m] = (unsigned)(((r * NA + a) * RH + 2 * cp) * 8);
+        dst[m] = valid ? reinterpret_cast<float2*>((a ? dst1 : dst0) + r * RH) + cp
+                       : reinterpret_cast<float2*>(sink);
+    }
+    return poll_couples<M>(xr, off, so, seq, dst, ctl);
+}
+
+}  // namespace
+
+template <int NR>
+__global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    const int tid = threadIdx.x;
+    // ---- group formation (as kernels_persist.hip) -------------------------------------------
+    if (tid == 0) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        const int g = x & 7;
+        s_group = g;
+        s_slot = (int)atomicAdd(a.ctl + PC_REG + g, 1u);
+        atomicAdd(a.ctl + PC_TOTAL, 1u);
+        const unsigned t0 = p_now();
+        int ok = 1;
+        while (ld_sc1_u(a.ctl + PC_TOTAL) < (unsigned)(kPG * kPM)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (p_now() - t0 > kSpinTicks) {
+                ok = 0;
+                atomicMax(a.ctl + PC_ERR, 1u);
+                break;
+            }
+        }
+        if (ok)
+            for (int i = 0; i < kPG; ++i)
+                if (ld_sc1_u(a.ctl + PC_REG + i) != (unsigned)kPM) {
+                    ok = 0;
+                    atomicMax(a.ctl + PC_ERR, 3u);
+                }
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    const int g0 = a.rb + g;                  // first fold row of this group in this launch
+    const int q = tid >> 7;                   // quad (wave-uniform)
+    const int og = (tid >> 4) & 7, kc = tid & 15;
+    const int u = RU * w + og;                // unit / output of this thread's weight rows
+    const int cl = 8 * q + og;                // fc5 class of this thread within the slot
+    const int cls = a.cpw * w + cl;
+    const bool has_cls = cl < a.cpw && cls < a.n_classes;
+    const int j = tid & (RH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
+    constexpr int NRH = (NR + 1) / 2;
+    unsigned* fl = a.flags + (size_t)g * 4 * 64;
+    const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * RX_GROUP);
+
+    // ---- weights -------------------------------------------------------------------------
+    float4 wr[kRNW];
+    {
+        const float4* src = a.wreg + ((size_t)w * kPT + tid) * kRNW;
+#pragma unroll
+        for (int i = 0; i < kRNW; ++i) wr[i] = src[i];
+        const float4* s5 = a.w5 + (size_t)w * 32 * RK4;
+        float4* d5 = reinterpret_cast<float4*>(lds + L_W5);
+        for (int i = tid; i < 32 * RK4; i += kPT) d5[i] = s5[i];
+    }
+    // ---- chunk state ----------------------------------------------------------------------
+    const size_t SW = 11 * RH;  // state floats per row
+    float h1[NRH];
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+        const int r = 2 * i + hs;
+        h1[i] = 0.f;
+        if (r < NR) {
+            const float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+            h1[i] = st[RH + j];
+            lds[L_XA + r * RH + j] = st[j];
+            lds[L_H1 + r * RH + j] = h1[i];
+            lds[L_H4 + r * RH + j] = st[4 * RH + j];
+        }
+    }
+    const bool own = kc < NR;  // lane kc owns (unit u, row kc) in the epilogues
+    const int lr = own ? kc : 0;
+    const int lrow = g0 + kPG * lr;
+    float h2r = 0.f, h3r = 0.f, h4r = 0.f;
+    if (own) {
+        const float* st = a.st + (size_t)lrow * SW;
+        if (q == 0) {
+            h2r = st[2 * RH + u];
+            h3r = st[3 * RH + u];
+#pragma unroll
+            for (int jg = 0; jg < 3; ++jg) {
+                lds[L_GH2 + (jg * RU + og) * kRNR + kc] = st[5 * RH + jg * RH + u];
+                lds[L_GH3 + (jg * RU + og) * kRNR + kc] = st[8 * RH + jg * RH + u];
+            }
+        } else if (q == 1) {
+            h4r = st[4 * RH + u];
+        }
+    }
+    if (tid < 24) {
+        const int jg = tid >> 3, ul = tid & 7, uu = jg * RH + RU * w + ul;
+        lds[L_CB + CB_IH2 + tid] = a.b_ih2[uu];
+        lds[L_CB + CB_IH4 + tid] = a.b_ih4[uu];
+        lds[L_CB + CB_HH1 + tid] = a.b_hh1[uu];
+        lds[L_CB + CB_HH2 + tid] = a.b_hh2[uu];
+        lds[L_CB + CB_HH3 + tid] = a.b_hh3[uu];
+        lds[L_CB + CB_HH4 + tid] = a.b_hh4[uu];
+        if (tid < 8) {
+            lds[L_CB + CB_F2 + tid] = a.b_f2[RU * w + tid];
+            lds[L_CB + CB_F4 + tid] = a.b_f4[RU * w + tid];
+        }
+    }
+    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid == 0) lds[L_FAIL] = 0.f;
+    const float vj0 = a.v[j], vj1 = a.v[RH + j], vj2 = a.v[2 * RH + j], w0j = a.w0[j];
+    const float bcls = has_cls ? a.b_f5[cls] : 0.f;
+    const rsrc_t fcr = mk_rsrc(a.fcond);
+    const unsigned o_tid = (unsigned)j * 4u;
+    __syncthreads();
+
+    const float4* XA = reinterpret_cast<const float4*>(lds + L_XA);
+    const float4* XB = reinterpret_cast<const float4*>(lds + L_XB);
+    float* sink = lds + L_DUMMY;
+    const int wave = tid >> 6;
+    // GRU hop k (0: x2/h2, 1: x3/h3, 2: x4/h4) pair (row lr, array, unit u); fc hop k pair
+    const unsigned o_gx = (unsigned)((lr * 2) * RH + u) * 8u, o_gh = o_gx + RH * 8u;
+    const unsigned o_f = (unsigned)(lr * RH + u) * 8u;
+    auto sg = [](int k) { return (unsigned)(RX_G + k * RX_G_SZ) * 4u; };
+    auto sf = [](int k) { return (unsigned)(RX_F + k * RX_F_SZ) * 4u; };
+
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
+    for (int t = a.t0; t < a.t1; ++t) {
+        const unsigned seq = (unsigned)t + 1u;
+        const bool nxt = t + 1 < a.S;
+        const unsigned par = (unsigned)(t & 1);
+        // ---- per-step conditioning / noise loads, consumed later in this step ----------------
+        float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f;
+        if (own) {
+            const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
+            const unsigned fo = (unsigned)(p_frame(lri, t, a.hop) * a.cond_width) * 4u;
+            if (q == 0) {  // GRU3: W_ih3[:, 256:] a2 + b_ih3
+                const unsigned o = (unsigned)(a.oG3 + u) * 4u + fo;
+                pc0 = bld(fcr, o, 0);
+                pc1 = bld(fcr, o, RH * 4);
+                pc2 = bld(fcr, o, 2 * RH * 4);
+            } else if (q == 1) {  // fc3: fc3[:, 256:] a4 + b
+                pc0 = bld(fcr, (unsigned)(a.oF3 + u) * 4u + fo, 0);
+            } else if (q == 3) {  // fc1: fc1[:, 256:] a3 + b
+                pc0 = bld(fcr, (unsigned)(a.oF1 + u) * 4u + fo, 0);
+            }
+        }
+        const float* cb = lds + L_CB;
+        // ================= stage 1: q0 GRU2 | q1 gh1 (published) | q3 gh4 (local) ==========
+        if (q == 0) {
+            __builtin_amdgcn_s_setprio(2);
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 0>(wr, XA, kc, s0, s1, s2);
+            if (own) {
+                const float* gh = lds + L_GH2 + og * kRNR + kc;
+                const float hn = p_gru(p_add(s0, cb[CB_IH2 + og]), p_add(s1, cb[CB_IH2 + 8 + og]),
+                                       p_add(s2, cb[CB_IH2 + 16 + og]), gh[0], gh[RU * kRNR],
+                                       gh[2 * RU * kRNR], h2r);
+                h2r = hn;
+                bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(0));
+                bst_tag(hn, seq, xr, o_gh, sg(0));
+            }
+            __builtin_amdgcn_s_setprio(0);
+        } else if (q == 1) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H1), kc, s0, s1, s2);
+            if (own) {
+                const unsigned o = (unsigned)((par * kRNR + kc) * 3 * RH + u) * 4u;
+                const unsigned so = (unsigned)RX_GH1 * 4u;
+                bst(p_add(s0, cb[CB_HH1 + og]), xr, o, so);
+                bst(p_add(s1, cb[CB_HH1 + 8 + og]), xr, o + RH * 4, so);
+                bst(p_add(s2, cb[CB_HH1 + 16 + og]), xr, o + 2 * RH * 4, so);
+            }
+            // gh1 reaches L2 before this wave's later publishes (GRU4 at stage 3): a consumer
+            // that has seen every slot's x4/h4 tags reads gh1 with plain loads
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (q == 3) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 0>(wr, reinterpret_cast<const float4*>(lds + L_H4), kc, s0, s1, s2);
+            if (own) {
+                float* gh = lds + L_GH4 + og * kRNR + kc;
+                gh[0] = p_add(s0, cb[CB_HH4 + og]);
+                gh[RU * kRNR] = p_add(s1, cb[CB_HH4 + 8 + og]);
+                gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH4 + 16 + og]);
+            }
+        }
+        if (!poll_hop<NR, 2>(xr, sg(0), seq, lds + L_XB, lds + L_H2, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 2: q0 GRU3 | q2 gh2 (next step) ============================
+        if (q == 0) {
+            __builtin_amdgcn_s_setprio(2);
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 12>(wr, XB, kc, s0, s1, s2);
+            if (own) {
+                const float* gh = lds + L_GH3 + og * kRNR + kc;
+                const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2), gh[0],
+                                       gh[RU * kRNR], gh[2 * RU * kRNR], h3r);
+                h3r = hn;
+                bst_tag(p_add(lds[L_XB + kc * RH + u], hn), seq, xr, o_gx, sg(1));
+                bst_tag(hn, seq, xr, o_gh, sg(1));
+            }
+            __builtin_amdgcn_s_setprio(0);
+        } else if (q == 2) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 0>(wr, reinterpret_cast<const float4*>(lds + L_H2), kc, s0, s1, s2);
+            if (own) {
+                float* gh = lds + L_GH2 + og * kRNR + kc;
+                gh[0] = p_add(s0, cb[CB_HH2 + og]);
+                gh[RU * kRNR] = p_add(s1, cb[CB_HH2 + 8 + og]);
+                gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH2 + 16 + og]);
+            }
+        }
+        if (!poll_hop<NR, 2>(xr, sg(1), seq, lds + L_XA, lds + L_H3, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 3: q1 GRU4 | q2 gh3 (next step) ============================
+        if (q == 1) {
+            __builtin_amdgcn_s_setprio(2);
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 0>(wr, XA, kc, s0, s1, s2);
+            if (own) {
+                const float* gh = lds + L_GH4 + og * kRNR + kc;
+                const float hn = p_gru(p_add(s0, cb[CB_IH4 + og]), p_add(s1, cb[CB_IH4 + 8 + og]),
+                                       p_add(s2, cb[CB_IH4 + 16 + og]), gh[0], gh[RU * kRNR],
+                                       gh[2 * RU * kRNR], h4r);
+                h4r = hn;
+                bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(2));
+                bst_tag(hn, seq, xr, o_gh, sg(2));
+            }
+            __builtin_amdgcn_s_setprio(0);
+        } else if (q == 2) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H3), kc, s0, s1, s2);
+            if (own) {
+                float* gh = lds + L_GH3 + og * kRNR + kc;
+                gh[0] = p_add(s0, cb[CB_HH3 + og]);
+                gh[RU * kRNR] = p_add(s1, cb[CB_HH3 + 8 + og]);
+                gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH3 + 16 + og]);
+            }
+        }
+        if (!poll_hop<NR, 2>(xr, sg(2), seq, lds + L_XB, lds + L_H4, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // GRU1 operands of the end of this step: every slot's gh1 is in L2 (drained before its
+        // x4/h4 publish, all of which this workgroup has seen)
+        float pG[NRH][3];
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) {
+            const int r = 2 * i + hs < NR ? 2 * i + hs : 0;
+#pragma unroll
+            for (int jg = 0; jg < 3; ++jg)
+                pG[i][jg] = bld_nt(xr, o_tid, (unsigned)(RX_GH1 + (par * kRNR + r) * 3 * RH + jg * RH) * 4u);
+        }
+        // P1 / cI of step t+1 for the same GRU1 (HBM latency hides behind stages 4-8)
+        float pP[NRH][3], pC[NRH];
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) pP[i][0] = pP[i][1] = pP[i][2] = pC[i] = 0.f;
+        if (nxt) {
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(t + 1) * a.B + g0) * 3 * RH);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(t + 1) * a.B + g0) * RH);
+#pragma unroll
+            for (int i = 0; i < NRH; ++i) {
+                const int r = 2 * i + hs;
+                if (r < NR) {
+#pragma unroll
+                    for (int jg = 0; jg < 3; ++jg)
+                        pP[i][jg] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * RH + jg * RH) * 4u);
+                    pC[i] = bld(cr, o_tid, (unsigned)(r * kPG * RH) * 4u);
+                }
+            }
+        }
+        float pgum = 0.f;  // Gumbel noise of (row kc, class cls), step t
+        if (own && has_cls && a.mode == 0)
+            pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
+                       (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+        // ================= stage 4: q3 fc1 ==================================================
+        if (q == 3) {
+            __builtin_amdgcn_s_setprio(2);
+            const float s = mv1<NR, 12>(wr, XB, kc);
+            if (own) bst_tag(p_add(s, pc0), seq, xr, o_f, sf(0));
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (!poll_hop<NR, 1>(xr, sf(0), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 5: q2 fc2 (relu) ===========================================
+        if (q == 2) {
+            __builtin_amdgcn_s_setprio(2);
+            const float s = mv1<NR, 24>(wr, XA, kc);
+            if (own) {
+                const float y = p_add(s, cb[CB_F2 + og]);
+                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_f, sf(1));
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (!poll_hop<NR, 1>(xr, sf(1), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 6: q1 fc3 ==================================================
+        if (q == 1) {
+            __builtin_amdgcn_s_setprio(2);
+            const float s = mv1<NR, 24>(wr, XB, kc);
+            if (own) bst_tag(p_add(s, pc0), seq, xr, o_f, sf(2));
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (!poll_hop<NR, 1>(xr, sf(2), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 7: q0 fc4 (relu) ===========================================
+        if (q == 0) {
+            __builtin_amdgcn_s_setprio(2);
+            const float s = mv1<NR, 24>(wr, XA, kc);
+            if (own) {
+                const float y = p_add(s, cb[CB_F4 + og]);
+                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_f, sf(3));
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (!poll_hop<NR, 1>(xr, sf(3), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 8: fc5 -> per-slot candidates (RAW) / logits (MOL) =========
+        {
+            float s0 = 0.f;
+            if (8 * q < a.cpw) {  // wave-uniform skip of idle quads
+                const float4* W5 = reinterpret_cast<const float4*>(lds + L_W5) + cl * RK4;
+                float4 w5[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w5[i] = W5[16 * i + kc];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    v2f acc = {0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) dot4(acc, w5[i], XB[r * RK4 + 16 * i + kc]);
+                    const float tt = row16_sum(hsum(acc));
+                    if (kc == r) s0 = tt;
+                }
+            }
+            float* red = lds + L_RED;  // [cl][r][value, class]
+            if (own) {
+                float val = -INFINITY;
+                if (has_cls) {
+                    const float l = p_add(s0, bcls);
+                    if (a.mode == 0)
+                        val = p_add(l, pgum);
+                    else
+                        bst(l, xr, (unsigned)(kc * 32 + cls) * 4u, (RX_D + RX_D_LOG) * 4);
+                }
+                red[(cl * kRNR + kc) * 2] = val;
+                red[(cl * kRNR + kc) * 2 + 1] = __int_as_float(cls);
+            }
+            __syncthreads();
+            if (wave == 0) {
+                if (a.mode == 0) {
+                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
+                        const int r = tid >> 4, o = tid & 15;
+                        float bv = -INFINITY;
+                        int bi = 0x7fffffff;
+                        if (r < NR && o < a.cpw) {
+                            bv = red[(o * kRNR + r) * 2];
+                            bi = __float_as_int(red[(o * kRNR + r) * 2 + 1]);
+                        }
+                        row16_argmax(bv, bi);
+                        if (r < NR && o == 0)
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
+                    } else {
+#pragma unroll
+                        for (int rb = 0; rb < NR; rb += 2) {
+                            const int r = rb + (tid >> 5), o = tid & 31;
+                            float bv = -INFINITY;
+                            int bi = 0x7fffffff;
+                            if (r < NR && o < a.cpw) {
+                                bv = red[(o * kRNR + r) * 2];
+                                bi = __float_as_int(red[(o * kRNR + r) * 2 + 1]);
+                            }
+                            half_argmax(bv, bi);
+                            if (r < NR && o == 31)
+                                __builtin_amdgcn_raw_buffer_store_b64(
+                                    (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                    (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
+                        }
+                    }
+                } else {  // MOL: logits rows + flag
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (tid == 0)
+                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
+        // ================= sample of step t (redundant in every workgroup) ==================
+        if (a.mode == 0) {
+            if (tid < 32 * NR) {  // half-wave r: lane o polls slot o's tagged candidate of row r
+                const int r = tid >> 5, o = tid & 31;
+                const unsigned off = (unsigned)((o * kRNR + r) * 2) * 4u;
+                const unsigned want = seq & kTagSeqMask;
+                u2v c;
+                const unsigned ts = p_now();
+                unsigned n = 0;
+                while (true) {
+                    c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, RX_D * 4, kCpNT);
+                    if (__all((c.y >> 11) == want)) break;
+                    if ((++n & 255) == 0) {
+                        if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - ts > kSpinTicks) {
+                            if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                            lds[L_FAIL] = 1.f;
+                            break;
+                        }
+                    }
+                }
+                float bv = __uint_as_float(c.x);
+                int bi = (int)(c.y & 0x7ffu);
+                half_argmax(bv, bi);
+                if (o == 31) {
+                    float xv;
+                    {
+#pragma clang fp contract(off)
+                        xv = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
+                    }
+                    lds[L_SX + r] = xv;
+                    if (w == 0) {
+                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
+                                                              ro * 2u, (unsigned)t * 2u, 0);
+                        bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                    }
+                }
+            }
+        } else if (tid < NR) {
+            // MOL: vocoder/distribution.py:104-140 with the precomputed draws of k_mol_noise
+            const int r = tid, row = g0 + kPG * r;
+            const unsigned lo = (unsigned)(r * 32) * 4u;
+            const unsigned so = (RX_D + RX_D_LOG) * 4;
+            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
+            float gm[11];
+#pragma unroll
+            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
+            float xv;
+            {
+#pragma clang fp contract(off)
+                float bv = -INFINITY;
+                int bi = 0;
+#pragma unroll
+                for (int k = 0; k < 10; ++k) {
+                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
+                    if (v2 > bv) {
+                        bv = v2;
+                        bi = k;
+                    }
+                }
+                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
+                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
+                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                ls = ls < lsmin ? lsmin : ls;
+                xv = mean + expf(ls) * gm[10];
+                xv = xv < -1.f ? -1.f : xv;
+                xv = xv > 1.f ? 1.f : xv;
+            }
+            lds[L_SX + r] = xv;
+            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+        }
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        if (!nxt) continue;
+        // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) {
+            const int r = 2 * i + hs;
+            if (r < NR) {
+                const float x = lds[L_SX + r];
+                const float hn = p_gru(fmaf(vj0, x, pP[i][0]), fmaf(vj1, x, pP[i][1]),
+                                       fmaf(vj2, x, pP[i][2]), pG[i][0], pG[i][1], pG[i][2], h1[i]);
+                h1[i] = hn;
+                lds[L_XA + r * RH + j] = p_add(fmaf(w0j, x, pC[i]), hn);
+                lds[L_H1 + r * RH + j] = hn;
+            }
+        }
+        __syncthreads();
+    }
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+    // ---- save the chunk state ----------------------------------------------------------------
+    if (a.t1 < a.S) {
+        if (w == 0)
+#pragma unroll
+            for (int i = 0; i < NRH; ++i) {
+                const int r = 2 * i + hs;
+                if (r < NR) {
+                    float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+                    st[j] = lds[L_XA + r * RH + j];
+                    st[RH + j] = lds[L_H1 + r * RH + j];
+                }
+            }
+        if (own) {
+            float* st = a.st + (size_t)lrow * SW;
+            if (q == 0) {
+                st[2 * RH + u] = h2r;
+                st[3 * RH + u] = h3r;
+#pragma unroll
+                for (int jg = 0; jg < 3; ++jg) {
+                    st[5 * RH + jg * RH + u] = lds[L_GH2 + (jg * RU + og) * kRNR + kc];
+                    st[8 * RH + jg * RH + u] = lds[L_GH3 + (jg * RU + og) * kRNR + kc];
+                }
+            } else if (q == 1) {
+                st[4 * RH + u] = h4r;
+            }
+        }
+    }
+}
+
+// Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0); h2 = h3 = h4 = 0,
+// gh2 = b_hh2, gh3 = b_hh3.
+__global__ __launch_bounds__(kRH) void k_persist_rr_init(PersistRRArgs a) {
+    const int row = blockIdx.x, j = threadIdx.x, H = kRH;
+    const float* P1 = a.P1 + (size_t)row * 3 * H;  // step 0
+    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
+                           a.b_hh1[2 * H + j], 0.f);
+    float* st = a.st + (size_t)row * 11 * H;
+    st[j] = p_add(a.cI[(size_t)row * H + j], hn);
+    st[H + j] = hn;
+    st[2 * H + j] = 0.f;
+    st[3 * H + j] = 0.f;
+    st[4 * H + j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        st[5 * H + k * H + j] = a.b_hh2[k * H + j];
+        st[8 * H + k * H + j] = a.b_hh3[k * H + j];
+    }
+}
+
+hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_persist_rr_init, dim3(a.B), dim3(kRH), 0, s, a);
+    return hipGetLastError();
+}
+
+size_t persist_rr_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
+size_t persist_rr_xbuf_floats() { return (size_t)kPG * RX_GROUP; }
+
+template <int NR>
+hipError_t launch_persist_rr_t(const PersistRRArgs& a, hipStream_t s) {
+    static bool attr = false;
+    const size_t lds = persist_rr_lds_bytes();
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_rr<NR>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_persist_rr<NR>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NR>
+int persist_rr_spill_t() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+int persist_rr_variant_ok(int nr, int cpw) {
+    if (cpw < 1 || cpw > 32) return 0;
+    int sp = -1;
+    switch (nr) {
+        case 1: sp = persist_rr_spill_t<1>(); break;
+        case 2: sp = persist_rr_spill_t<2>(); break;
+        case 3: sp = persist_rr_spill_t<3>(); break;
+        case 4: sp = persist_rr_spill_t<4>(); break;
+        default: break;
+    }
+    return sp == 0 ? 1 : 0;
+}
+
+hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s) {
+    if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > 32 ||
+        a.cpw * kPM < a.n_classes || (a.mode != 0 && a.n_classes > 32))
+        return hipErrorInvalidValue;
+    switch (a.nr) {
+        case 1: return launch_persist_rr_t<1>(a, s);
+        case 2: return launch_persist_rr_t<2>(a, s);
+        case 3: return launch_persist_rr_t<3>(a, s);
+        case 4: return launch_persist_rr_t<4>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace wrnn

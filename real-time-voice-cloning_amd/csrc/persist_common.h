@@ -1,0 +1,206 @@
+// Device helpers shared by the persistent recurrence kernels (kernels_persist.hip: fatchord,
+// kernels_persist_rr.hip: runtimeracer): timers, DPP reductions, gate nonlinearities, buffer
+// resource access, tagged-pair exchanges over the XCD-shared L2.
+#pragma once
+#include "wrnn_kernels.h"
+
+namespace wrnn {
+
+constexpr unsigned kSpinTicks = 100000000u;  // 1 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ unsigned p_now() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned ld_nt_u(const unsigned* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float ld_nt_f(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float4 ld_nt_f4(const float4* p) {
+    const float* q = reinterpret_cast<const float*>(p);
+    return make_float4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
+                       __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
+}
+__device__ __forceinline__ unsigned ld_sc1_u(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float pdpp(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 16 lanes of a DPP row; every lane of the row receives the same total
+__device__ __forceinline__ float row16_sum(float v) {
+    v += pdpp<0xB1>(v);   // quad_perm xor 1
+    v += pdpp<0x4E>(v);   // quad_perm xor 2
+    v += pdpp<0x124>(v);  // row_ror 4
+    v += pdpp<0x128>(v);  // row_ror 8
+    return v;
+}
+
+// Gate nonlinearities on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each):
+// sigmoid(x) = 1 / (1 + 2^(-x log2 e)), tanh(x) = 1 - 2 / (2^(2x log2 e) + 1). Within a few ulp
+// of torch's vectorised sigmoid / tanh -- the same order as the fp32 summation-order
+// differences of the matrix products -- at a fraction of the cost of expf / IEEE division /
+// tanhf; the RAW label parity tests run on this path.
+__device__ __forceinline__ float p_sigmoid(float x) {
+    const float e = __builtin_amdgcn_exp2f(-x * 1.4426950408889634f);
+    return __builtin_amdgcn_rcpf(1.0f + e);
+}
+__device__ __forceinline__ float p_tanh(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+// torch GRUCell gate arithmetic (same operation order as kernels_step.hip gru_cell)
+__device__ __forceinline__ float p_gru(float gi_r, float gi_z, float gi_n, float gh_r, float gh_z,
+                                       float gh_n, float h) {
+#pragma clang fp contract(off)
+    const float r = p_sigmoid(gh_r + gi_r);
+    const float z = p_sigmoid(gh_z + gi_z);
+    const float ghr = gh_n * r;
+    const float n = p_tanh(gi_n + ghr);
+    const float d = h - n;
+    const float dz = d * z;
+    return dz + n;
+}
+__device__ __forceinline__ float p_add(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+
+// packed fp32 (v_pk_fma_f32): even/odd-k partial sums of one (output, row) dot product
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void dot4(v2f& acc, const float4 w, const float4 x) {
+    acc = __builtin_elementwise_fma((v2f){w.x, w.y}, (v2f){x.x, x.y}, acc);
+    acc = __builtin_elementwise_fma((v2f){w.z, w.w}, (v2f){x.z, x.w}, acc);
+}
+__device__ __forceinline__ float hsum(const v2f a) { return a.x + a.y; }
+
+__device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
+    const int rel = ri.rel0 + t;
+    return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
+}
+
+__device__ __forceinline__ bool p_wait(const unsigned* f, unsigned target, unsigned* ctl, int tid) {
+    // wave 0 polls the group's 32 flags; every wave then meets at the barrier
+    __shared__ int s_fail;
+    if (tid < 64) {
+        const unsigned t0 = p_now();
+        unsigned n = 0;
+        bool ok = true;
+        while (true) {
+            const unsigned v = tid < kPM ? ld_nt_u(f + tid) : target;
+            if (__all(v >= target)) break;
+            if ((++n & 255) == 0) {
+                if (ld_sc1_u(ctl + PC_ERR)) {
+                    ok = false;
+                    break;
+                }
+                if (p_now() - t0 > kSpinTicks) {
+                    if (tid == 0) atomicMax(ctl + PC_ERR, 2u);
+                    ok = false;
+                    break;
+                }
+            }
+        }
+        if (tid == 0) s_fail = ok ? 0 : 1;
+    }
+    __syncthreads();
+    return s_fail == 0;
+}
+
+__device__ __forceinline__ void p_publish(unsigned* flag, unsigned value, int tid) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int CTRL>
+__device__ __forceinline__ int pdpp_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp_step(float& v, int& k) {
+    const float v2 = pdpp<CTRL>(v);
+    const int k2 = pdpp_i<CTRL>(k);
+    if (v2 > v || (v2 == v && k2 < k)) {
+        v = v2;
+        k = k2;
+    }
+}
+// argmax over the 16 lanes of a DPP row (value, class); ties -> lowest class; all lanes get it
+__device__ __forceinline__ void row16_argmax(float& v, int& k) {
+    amax_dpp_step<0xB1>(v, k);
+    amax_dpp_step<0x4E>(v, k);
+    amax_dpp_step<0x124>(v, k);
+    amax_dpp_step<0x128>(v, k);
+}
+
+// RAW hop D carries its own sequence tag: each slot writes one 64-bit word per row,
+// (value bits, step << 11 | class), so consumers poll the candidates themselves.
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+constexpr unsigned kTagSeqMask = (1u << 21) - 1;  // steps per call < 2^21 (host-checked)
+
+// argmax over the 32 lanes of a half-wave (value, class); ties -> lowest class. DPP only:
+// each 16-lane row reduces itself, then row_bcast:15 hands row 0's (row 2's) result to row 1
+// (row 3). The half-wave's result is valid in its upper 16 lanes (lane & 31 >= 16).
+__device__ __forceinline__ void half_argmax(float& v, int& k) {
+    row16_argmax(v, k);
+    const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x142, 0xA, 0xF, false));
+    const int k2 = __builtin_amdgcn_update_dpp(k, k, 0x142, 0xA, 0xF, false);
+    if (v2 > v || (v2 == v && k2 < k)) {
+        v = v2;
+        k = k2;
+    }
+}
+
+// Buffer-resource access: a uniform (SGPR) base and a 32-bit per-lane byte offset, so no
+// 64-bit per-lane addresses stay live across the step loop.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kCpNT = 2;  // cache policy: non-temporal (served by L2, bypasses the CU's L1)
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float bld(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ float bld_nt(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kCpNT));
+}
+__device__ __forceinline__ float4 bld4_nt(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kCpNT));
+}
+__device__ __forceinline__ void bst(float v, rsrc_t r, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bst_tag(float v, unsigned tag, rsrc_t r, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(v), tag}, r, voff, soff, 0);
+}
+// Poll M 16-byte couples (two tagged pairs each) until every tag equals `want`, storing the
+// values to LDS (dst[m], float2) on every pass; the last pass, the one that saw all tags, wins.
+// False on an abort / timeout (error code set).
+template <int M>
+__device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M], unsigned so,
+                                             unsigned want, float2* const (&dst)[M], unsigned* ctl) {
+    // spin on the first couple only (a thread's couples all come from one producer slot), then
+    // take the whole set and verify every tag; keeps the polling traffic in L2 small
+    const unsigned t0 = p_now();
+    unsigned n = 0;
+    while (true) {
+        const u4v c0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off[0], so, kCpNT);
+        if (__all(c0.y == want && c0.w == want)) {
+            bool ok = true;
+            *dst[0] = make_float2(__uint_as_float(c0.x), __uint_as_float(c0.z));
+#pragma unroll
+            for (int m = 1; m < M; ++m) {
+                const u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off[m], so, kCpNT);
+                *dst[m] = make_float2(__uint_as_float(c.x), __uint_as_float(c.z));
+                ok = ok && c.y == want && c.w == want;
+            }
+            if (__all(ok)) return true;
+        }
+        if ((++n & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
+            if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
+            return false;
+        }
+    }
+}
+
+}  // namespace wrnn

@@ -170,11 +170,14 @@ struct wrnn_handle {
 
     // ---- persistent engine (kernels_persist.hip)
     struct PersistW {
-        bool ok = false;  // weights packed: fatchord, rnn_dims = fc_dims = 512, n <= 1024
-        int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;
+        bool ok = false;  // weights packed (fatchord 512 / runtimeracer 256 dims, n <= 1024)
+        bool rr = false;  // runtimeracer topology (kernels_persist_rr.hip)
+        int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;  // rr: oG2 = oG3, oF2 = oF3
         const float *wreg = nullptr, *wlds = nullptr;
         const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
-        const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;
+        const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
+        const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
+                    *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
     } pw;
     struct PersistWS {
         DevBuf P1, gumbel, ctl, flags, xbuf, st, stamps, phases;
@@ -337,6 +340,45 @@ std::vector<float> transpose_cols(const std::vector<float>& W, int rows, int ld,
 //   24..31 fc2 row u (og < 16) or fc1 row u (og >= 16), x part only
 //   32..39 fc3 row cpw w + og when a slot owns more than 16 classes
 // and in LDS: W_hh2 rows [16 units][3 gates][128 float4], then fc3 rows [16][128 float4].
+// P1 = W_ih1 (I[:,1:] c + b_I) + b_ih1 = M1 c + bP1 with M1 = W_ih1 I[:,1:] (f64 products):
+// one K = feat + A - 1 contraction per (step, row) instead of K = rnn_dims (both topologies
+// feed rnn1 with I(x0), fatchord_version.py:198-201, runtimeracer_version.py:248-252)
+int pack_p1(wrnn_handle* h) {
+    auto& T = h->host;
+    auto& P = h->pw;
+    const int H = h->H, A = h->A;
+    int rc = WRNN_OK;
+    {
+        const auto& Wih1 = T["rnn1.weight_ih_l0"];  // (3H, H)
+        const auto& WI = T["I.weight"];             // (H, feat + A)
+        const auto& bI = T["I.bias"];
+        const auto& bih1 = T["rnn1.bias_ih_l0"];
+        const int ldI = h->feat + A, KI = h->KI;
+        std::vector<double> WIk((size_t)H * KI);
+        for (int j = 0; j < H; ++j)
+            for (int k = 0; k < KI; ++k) WIk[(size_t)j * KI + k] = WI[(size_t)j * ldI + 1 + k];
+        std::vector<float> M1T((size_t)KI * 3 * H), bP1(3 * H);
+        std::vector<double> acc(KI);
+        for (int o = 0; o < 3 * H; ++o) {
+            std::fill(acc.begin(), acc.end(), 0.0);
+            double b = bih1[o];
+            for (int j = 0; j < H; ++j) {
+                const double wv = Wih1[(size_t)o * H + j];
+                const double* row = &WIk[(size_t)j * KI];
+                for (int k = 0; k < KI; ++k) acc[k] += wv * row[k];
+                b += wv * (double)bI[j];
+            }
+            for (int k = 0; k < KI; ++k) M1T[(size_t)k * 3 * H + o] = (float)acc[k];
+            bP1[o] = (float)b;
+        }
+        P.M1T = upload(h, M1T, &rc);
+        CHECK(rc);
+        P.bP1 = upload(h, bP1, &rc);
+        CHECK(rc);
+    }
+    return WRNN_OK;
+}
+
 int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     auto& T = h->host;
     const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
@@ -393,36 +435,7 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     CHECK(rc);
     P.wlds = upload(h, wlds, &rc);
     CHECK(rc);
-    // P1 = W_ih1 (I[:,1:] c + b_I) + b_ih1 = M1 c + bP1 with M1 = W_ih1 I[:,1:] (f64 products):
-    // one K = feat + A - 1 contraction per (step, row) instead of K = rnn_dims
-    {
-        const auto& Wih1 = T["rnn1.weight_ih_l0"];  // (3H, H)
-        const auto& WI = T["I.weight"];             // (H, feat + A)
-        const auto& bI = T["I.bias"];
-        const auto& bih1 = T["rnn1.bias_ih_l0"];
-        const int ldI = h->feat + A, KI = h->KI;
-        std::vector<double> WIk((size_t)H * KI);
-        for (int j = 0; j < H; ++j)
-            for (int k = 0; k < KI; ++k) WIk[(size_t)j * KI + k] = WI[(size_t)j * ldI + 1 + k];
-        std::vector<float> M1T((size_t)KI * 3 * H), bP1(3 * H);
-        std::vector<double> acc(KI);
-        for (int o = 0; o < 3 * H; ++o) {
-            std::fill(acc.begin(), acc.end(), 0.0);
-            double b = bih1[o];
-            for (int j = 0; j < H; ++j) {
-                const double wv = Wih1[(size_t)o * H + j];
-                const double* row = &WIk[(size_t)j * KI];
-                for (int k = 0; k < KI; ++k) acc[k] += wv * row[k];
-                b += wv * (double)bI[j];
-            }
-            for (int k = 0; k < KI; ++k) M1T[(size_t)k * 3 * H + o] = (float)acc[k];
-            bP1[o] = (float)b;
-        }
-        P.M1T = upload(h, M1T, &rc);
-        CHECK(rc);
-        P.bP1 = upload(h, bP1, &rc);
-        CHECK(rc);
-    }
+    CHECK(pack_p1(h));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
@@ -434,6 +447,80 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     P.oG2 = oG2;
     P.oF1 = oF1;
     P.oF2 = oF2;
+    P.ok = true;
+    return WRNN_OK;
+}
+
+// Runtimeracer persistent-engine weight layout (kernels_persist_rr.hip). Slot w, thread tid
+// (quad q = tid / 128, og = (tid / 16) % 8, kc = tid % 16, unit u = 8 w + og) holds float4 i:
+//   gate block at b: b + 4 j + i = gate j of unit u, k-float4 16 i + kc
+//   fc block at b:   b + i       = row u, k-float4 16 i + kc
+//   quad 0: W_ih2 @0, W_ih3[:, :256] @12, fc4 @24      quad 1: W_ih4 @0, W_hh1 @12, fc3[:, :256] @24
+//   quad 2: W_hh2 @0, W_hh3 @12, fc2 @24               quad 3: W_hh4 @0, fc1[:, :256] @12
+// and w5 [slot][32][64 float4]: fc5 row cpw w + c of class c of the slot (LDS-resident).
+int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
+    auto& T = h->host;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    auto& P = h->pw;
+    P.ok = false;
+    P.rr = true;
+    if (h->cfg.model_type != WRNN_MODEL_RUNTIMERACER || H != kRH || F != kRH || n > kPM * 32)
+        return WRNN_OK;
+    P.cpw = (n + kPM - 1) / kPM;
+    P.nw = kRNW;
+    std::vector<float> wreg((size_t)kPM * kPT * kRNW * 4, 0.f);
+    for (int w = 0; w < kPM; ++w)
+        for (int tid = 0; tid < kPT; ++tid) {
+            const int q = tid >> 7, og = (tid >> 4) & 7, kc = tid & 15, u = 8 * w + og;
+            float* d = wreg.data() + ((size_t)w * kPT + tid) * kRNW * 4;
+            auto gate = [&](int b, const char* key, int ld) {
+                const auto& W = T[key];
+                for (int j = 0; j < 3; ++j)
+                    for (int i = 0; i < 4; ++i)
+                        std::memcpy(d + 4 * (b + 4 * j + i), &W[(size_t)(j * H + u) * ld + 4 * (16 * i + kc)],
+                                    4 * sizeof(float));
+            };
+            auto fc = [&](int b, const char* key, int ld, int row) {
+                const auto& W = T[key];
+                for (int i = 0; i < 4; ++i)
+                    std::memcpy(d + 4 * (b + i), &W[(size_t)row * ld + 4 * (16 * i + kc)], 4 * sizeof(float));
+            };
+            switch (q) {
+                case 0: gate(0, "rnn2.weight_ih_l0", H); gate(12, "rnn3.weight_ih_l0", H + A); fc(24, "fc4.weight", F, u); break;
+                case 1: gate(0, "rnn4.weight_ih_l0", H); gate(12, "rnn1.weight_hh_l0", H); fc(24, "fc3.weight", F + A, u); break;
+                case 2: gate(0, "rnn2.weight_hh_l0", H); gate(12, "rnn3.weight_hh_l0", H); fc(24, "fc2.weight", F, u); break;
+                default: gate(0, "rnn4.weight_hh_l0", H); fc(12, "fc1.weight", H + A, u); break;
+            }
+        }
+    std::vector<float> w5((size_t)kPM * 32 * kRH, 0.f);
+    for (int w = 0; w < kPM; ++w)
+        for (int cl = 0; cl < P.cpw; ++cl) {
+            const int c = P.cpw * w + cl;
+            if (c < n) std::memcpy(&w5[((size_t)w * 32 + cl) * kRH], &T["fc5.weight"][(size_t)c * F], F * sizeof(float));
+        }
+    int rc = WRNN_OK;
+    P.wreg = upload(h, wreg, &rc);
+    CHECK(rc);
+    P.wlds = upload(h, w5, &rc);
+    CHECK(rc);
+    CHECK(pack_p1(h));
+    auto dv = [&](const std::string& key) -> const float* {
+        if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
+        return h->dvec[key];
+    };
+    P.b_ih2 = dv("rnn2.bias_ih_l0");
+    P.b_ih4 = dv("rnn4.bias_ih_l0");
+    P.b_hh1 = dv("rnn1.bias_hh_l0");
+    P.b_hh2 = dv("rnn2.bias_hh_l0");
+    P.b_hh3 = dv("rnn3.bias_hh_l0");
+    P.b_hh4 = dv("rnn4.bias_hh_l0");
+    P.b_f2 = dv("fc2.bias");
+    P.b_f4 = dv("fc4.bias");
+    P.b_fc3 = dv("fc5.bias");
+    CHECK(rc);
+    P.oG2 = oG3;
+    P.oF1 = oF1;
+    P.oF2 = oF3;
     P.ok = true;
     return WRNN_OK;
 }
@@ -624,6 +711,7 @@ int do_finalize(wrnn_handle* h) {
         CHECK(pack_persist(h, oG2, oF1, oF2));
     } else {
         h->pw.ok = false;
+        h->pw.rr = false;
         const int oG3 = add_aux(1, "rnn3.weight_ih_l0", "rnn3.bias_ih_l0", 3 * H, H + A, H);
         const int oF1 = add_aux(2, "fc1.weight", "fc1.bias", F, H + A, H);
         const int oF3 = add_aux(3, "fc3.weight", "fc3.bias", F, F + A, F);
@@ -652,6 +740,7 @@ int do_finalize(wrnn_handle* h) {
         s7.segs.push_back(seg_fc("fc5", n, F, SL_Y4, SL_LOG, false, dv("fc5.bias"), -1));
         CHECK(rc);
         h->stages = {s0, s1, s2, s3, s4, s5, s6, s7};
+        CHECK(pack_persist_rr(h, oG3, oF1, oF3));
     }
     CHECK(rc);
     // per-frame cond pointers: mark with c_ld = -1 -> resolved against ws.fcond at launch
@@ -1196,7 +1285,7 @@ bool persist_device_ok(wrnn_handle* h) {
     hipDeviceProp_t p;
     bool ok = hipGetDeviceProperties(&p, d) == hipSuccess && p.multiProcessorCount == kPG * kPM &&
               std::strncmp(p.gcnArchName, "gfx950", 6) == 0 &&
-              p.sharedMemPerMultiprocessor >= persist_lds_bytes();
+              p.sharedMemPerMultiprocessor >= std::max(persist_lds_bytes(), persist_rr_lds_bytes());
     if (d >= 0 && d < 64) cached[d] = ok ? 1 : 2;
     return ok;
 }
@@ -1247,14 +1336,16 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     auto& ws = h->ws;
     auto& P = h->pws;
     const auto& W = h->pw;
-    const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;
+    const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;  // H: fatchord layout
     const bool raw = h->cfg.mode == WRNN_MODE_RAW;
     hipStream_t st = h->stream;
     CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
     CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
-    CHECK(P.xbuf.alloc(persist_xbuf_floats() * sizeof(float)));
-    CHECK(P.st.alloc((size_t)Bp * 6 * H * sizeof(float)));
+    const bool rr = W.rr;
+    const size_t xfl = rr ? persist_rr_xbuf_floats() : persist_xbuf_floats();
+    CHECK(P.xbuf.alloc(xfl * sizeof(float)));
+    CHECK(P.st.alloc((size_t)Bp * (rr ? 11 * kRH : 6 * H) * sizeof(float)));
     // P1 (all steps, rows) was written by run_upsample next to cI
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
     if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, (const RowInfo*)ws.rows.p, k0, k1, st));
@@ -1302,7 +1393,47 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(hipMemsetAsync(P.phases.p, 0, P.phases.bytes, st));
         a.phases = (uint32_t*)P.phases.p;
     }
-    HIPC(launch_persist_init(a, st));
+    PersistRRArgs ar{};
+    if (rr) {
+        ar.ctl = a.ctl;
+        ar.flags = a.flags;
+        ar.xbuf = a.xbuf;
+        ar.S = S;
+        ar.B = Bp;
+        ar.mode = a.mode;
+        ar.n_classes = n;
+        ar.hop = a.hop;
+        ar.cpw = W.cpw;
+        ar.rows = a.rows;
+        ar.wreg = (const float4*)W.wreg;
+        ar.w5 = (const float4*)W.wlds;
+        ar.b_ih2 = W.b_ih2;
+        ar.b_ih4 = W.b_ih4;
+        ar.b_hh1 = W.b_hh1;
+        ar.b_hh2 = W.b_hh2;
+        ar.b_hh3 = W.b_hh3;
+        ar.b_hh4 = W.b_hh4;
+        ar.b_f2 = W.b_f2;
+        ar.b_f4 = W.b_f4;
+        ar.b_f5 = W.b_fc3;
+        ar.v = h->v1;
+        ar.w0 = h->w0;
+        ar.fcond = a.fcond;
+        ar.cond_width = a.cond_width;
+        ar.oG3 = W.oG2;
+        ar.oF1 = W.oF1;
+        ar.oF3 = W.oF2;
+        ar.P1 = a.P1;
+        ar.cI = a.cI;
+        ar.gumbel = a.gumbel;
+        ar.labels = a.labels;
+        ar.samples = a.samples;
+        ar.ld = a.ld;
+        ar.st = P.st.f();
+        HIPC(launch_persist_rr_init(ar, st));
+    } else {
+        HIPC(launch_persist_init(a, st));
+    }
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
     // launches: row batches in order, each in time chunks (1000 steps when a progress callback
     // wants reports, else one chunk); the step tags restart with every batch, so the exchange
@@ -1335,7 +1466,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.t1 = std::min(S, a.t0 + G);
         if (c == 0) {
             HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
-            HIPC(hipMemsetAsync(P.xbuf.p, 0, persist_xbuf_floats() * sizeof(float), st));  // step tags
+            HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
         }
         // registration words only: an error code from an earlier launch stays visible
         HIPC(hipMemsetAsync(P.ctl.p, 0, PC_ERR * sizeof(unsigned), st));
@@ -1349,7 +1480,16 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             h->pev_steps.push_back(a.t1 - a.t0);
             HIPC(hipEventRecord(e0, st));
         }
-        HIPC(launch_persist(a, st));
+        if (rr) {
+            ar.t0 = a.t0;
+            ar.t1 = a.t1;
+            ar.nr = a.nr;
+            ar.rb = a.rb;
+            ar.stamps = a.stamps;
+            HIPC(launch_persist_rr(ar, st));
+        } else {
+            HIPC(launch_persist(a, st));
+        }
         if (h->timing) HIPC(hipEventRecord(e1, st));
         if (cb) {
             if (hipEventCreateWithFlags(&done[l], hipEventDisableTiming) != hipSuccess ||
@@ -1376,19 +1516,17 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     if (a.phase_t >= 0) persist_phase_report(h, a.phase_t);
     // algorithmic traffic per step: recurrent weights once + per row-step
     // conditioning (mel 80 + aux 128 floats) and the label
-    double wparams = 0;
-    for (const char* k : {"I.weight", "I.bias", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn1.bias_ih_l0",
-                          "rnn1.bias_hh_l0", "rnn2.weight_ih_l0", "rnn2.weight_hh_l0", "rnn2.bias_ih_l0",
-                          "rnn2.bias_hh_l0", "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias",
-                          "fc3.weight", "fc3.bias"})
-        wparams += (double)h->host[k].size();
+    // (every tensor of the step: I, rnn*, fc*; MACs: their weight matrices)
+    double wparams = 0, macs = 0;
+    for (const auto& kv : h->host) {
+        const std::string& k = kv.first;
+        if (k.rfind("I.", 0) && k.rfind("rnn", 0) && k.rfind("fc", 0)) continue;
+        wparams += (double)kv.second.size();
+        if (k.find("weight") != std::string::npos) macs += (double)kv.second.size();
+    }
     // per launch: one row batch (real rows averaged over the batches)
     const double rows_l = (double)B / nb;
     h->p_step_bytes = 4.0 * wparams + rows_l * ((h->feat + h->R) * 4.0 + 2.0);
-    double macs = 0;
-    for (const char* k : {"I.weight", "rnn1.weight_ih_l0", "rnn1.weight_hh_l0", "rnn2.weight_ih_l0",
-                          "rnn2.weight_hh_l0", "fc1.weight", "fc2.weight", "fc3.weight"})
-        macs += (double)h->host[k].size();
     h->p_step_flops = 2.0 * macs * rows_l;
     return WRNN_OK;
 }
@@ -1441,14 +1579,15 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     int nr_max = 0;
     if (h->pw.ok)
         for (int r = kPNR; r >= 1 && !nr_max; --r)
-            if (persist_variant_ok(r, h->pw.cpw)) nr_max = r;
+            if (h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw) : persist_variant_ok(r, h->pw.cpw)) nr_max = r;
     const int nbatch = nr_max ? (B + kPG * nr_max - 1) / (kPG * nr_max) : 0;
     const int nr = nbatch ? (B + kPG * nbatch - 1) / (kPG * nbatch) : 0;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
-        if (!h->pw.ok) why = "model is not fatchord with rnn_dims = fc_dims = 512 and <= 1024 classes";
+        if (!h->pw.ok)
+            why = "model is not fatchord (rnn_dims = fc_dims = 512) or runtimeracer (256) with <= 1024 classes";
         else if (!nr_max) why = "no register-resident variant for this class count";
-        else if ((double)S * kPG * nr * nbatch * (4 * kPH + h->n_classes) * 4.0 > kPersistWsBytes)
+        else if ((double)S * kPG * nr * nbatch * (4 * h->H + h->n_classes) * 4.0 > kPersistWsBytes)
             why = "P1 / noise workspace for " + std::to_string(B) + " rows x " + std::to_string(S) +
                   " steps exceeds " + std::to_string((long long)(kPersistWsBytes / (1 << 30))) + " GiB";
         else if (h->persist_failed) why = "a persistent launch failed earlier on this handle";

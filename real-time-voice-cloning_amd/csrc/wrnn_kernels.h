@@ -204,6 +204,55 @@ struct PersistArgs {
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
+// ---------------------------------------------------------------------------------------
+// Persistent runtimeracer recurrence (kernels_persist_rr.hip): rnn_dims = fc_dims = 256, four
+// GRUs and five linears per step. Same 8 XCD-local groups x 32 workgroups x 512 threads; a
+// workgroup owns 8 units / outputs of every layer and cpw classes of fc5; eight in-group hops
+// per step (GRU2, GRU3, GRU4, fc1, fc2, fc3, fc4, fc5 candidates).
+// ---------------------------------------------------------------------------------------
+constexpr int kRH = 256;     // rnn_dims == fc_dims
+constexpr int kRNR = 4;      // max fold rows per group and launch
+constexpr int kRNW = 28;     // float4 weight registers per thread
+
+struct PersistRRArgs {
+    unsigned* ctl;          // PC_WORDS control words
+    unsigned* flags;        // [kPG][4][64] (MOL hop flags)
+    float* xbuf;            // per-group exchange area (persist_rr_xbuf_floats())
+    int t0, t1, S;
+    int B, nr, rb;          // row stride, rows per group, first row of this launch's batch
+    int mode, n_classes, hop, cpw;
+    const RowInfo* rows;
+    const float4* wreg;     // [kPM][kPT][kRNW]
+    const float4* w5;       // [kPM][32][kRH / 4] fc5 rows of each slot (LDS-resident)
+    const float* b_ih2;     // [3H]
+    const float* b_ih4;     // [3H]
+    const float* b_hh1;     // [3H] ... b_hh4
+    const float* b_hh2;
+    const float* b_hh3;
+    const float* b_hh4;
+    const float* b_f2;      // [F]
+    const float* b_f4;      // [F]
+    const float* b_f5;      // [n]
+    const float* v;         // [3H] W_ih1 . w0
+    const float* w0;        // [H]
+    const float* fcond;     // per-frame conditioning rows
+    int cond_width, oG3, oF1, oF3;
+    const float* P1;        // [S][B][3H]
+    const float* cI;        // [S][B][H]
+    const float* gumbel;    // RAW [S][B][n]; MOL [S][B][kMolNoise]
+    int16_t* labels;        // [B][ld]
+    float* samples;         // [B][ld]
+    int ld;
+    float* st;              // chunk state [B][11 H]: x1, h1, h2, h3, h4 | gh2, gh3 (3H each)
+    uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
+};
+
+hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
+hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s);
+int persist_rr_variant_ok(int nr, int cpw);
+size_t persist_rr_lds_bytes();
+size_t persist_rr_xbuf_floats();
+
 hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, uint32_t k0,
                             uint32_t k1, hipStream_t s);
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,

@@ -48,14 +48,14 @@ def first_divergence(a, b):
 
 
 def engine_cases(mode):
-    # CHAIN runs every topology; PERSIST runs fatchord (rnn_dims = fc_dims = 512)
+    # both engines run both topologies (PERSIST: kernels_persist.hip for fatchord,
+    # kernels_persist_rr.hip for runtimeracer)
     out = []
     for k, v in golden_meta().items():
         if v['mode'] != mode:
             continue
         out.append((k, 'chain'))
-        if v['model_type'] == 'fatchord-wavernn':
-            out.append((k, 'persist'))
+        out.append((k, 'persist'))
     return out
 
 
@@ -117,8 +117,9 @@ def test_upsample_network_matches_oracle():
     np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize('case', ['fatchord_raw9_sharp_tiny', 'runtimeracer_raw9_tiny'])
 @pytest.mark.parametrize('n_utts', [3, 4, 6, 10])
-def test_persist_multi_row_groups_match_oracle(n_utts):
+def test_persist_multi_row_groups_match_oracle(n_utts, case):
     """5 fold rows per utterance -> 15 / 20 / 30 / 50 rows: 2 and 3 rows per XCD group (the
     padded-row variants of the persistent engine) and, past 24 rows, consecutive launches over
     row batches (30 rows -> 2 batches of 2 rows per group, 50 -> 3 batches of 3), every row
@@ -127,7 +128,7 @@ def test_persist_multi_row_groups_match_oracle(n_utts):
     from oracle.wavernn_oracle import oracle_infer_waveform
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    meta, _ = golden_case('fatchord_raw9_sharp_tiny')
+    meta, _ = golden_case(case)
     m, hp, sd = make_model(meta)
     mels = [synth_mel(meta['n_frames'], 100 + u) / sp.max_abs_value for u in range(n_utts)]
     dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
@@ -148,13 +149,14 @@ def test_persist_multi_row_groups_match_oracle(n_utts):
             f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'
 
 
-def test_persist_row_batches_mol_within_tolerance():
-    """MOL float path over two row batches (6 utterances x 5 rows = 30 rows)."""
+@pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny'])
+def test_persist_row_batches_mol_within_tolerance(case):
+    """MOL float path over row batches (6 utterances x the case's fold rows)."""
     import torch
     from oracle.wavernn_oracle import oracle_infer_waveform
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    meta, _ = golden_case('fatchord_mol_tiny')
+    meta, _ = golden_case(case)
     m, hp, sd = make_model(meta)
     n_utts = 6
     mels = [synth_mel(meta['n_frames'], 200 + u) / sp.max_abs_value for u in range(n_utts)]
