@@ -48,6 +48,25 @@ def parse():
     return ap.parse_args()
 
 
+def _pmc_traffic(kernel, workload):
+    try:
+        with open(os.path.join(REPO, 'profiles', 'pmc_traffic.json')) as f:
+            return json.load(f).get(f'{kernel}|{workload}')
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def cpu_baseline(args, sd, hp, mel):
     """Oracle (torch-CPU restatement of the reference generate) on a bounded sample."""
     import torch
@@ -64,6 +83,7 @@ def cpu_baseline(args, sd, hp, mel):
     t_total = r['t_prepare'] + r['t_loop'] * S / r['steps']
     samples = (args.frames - 1) * 200
     return dict(value=samples / t_total, unit='samples/s', cores=cores, kind='port',
+                cpu_model=_cpu_model(), affinity_cpus=len(os.sched_getaffinity(0)),
                 sample=f"oracle.wavernn_oracle (torch-CPU restatement of reference generate()), "
                        f"{args.model} {args.mode} {args.bits}-bit, T={args.frames}: upsample + first "
                        f"{r['steps']} of {S} steps ({r['B']} folds), loop time extrapolated to all "
@@ -126,6 +146,8 @@ def main():
     total_samples = samples_per_step * args.steps * world
     value = total_samples / dt
 
+    workload = (f'{U}x{args.frames}-frame mel per GPU, {args.model} {args.mode} {args.bits}-bit mu-law, '
+                f'batched folds target={args.target} overlap={args.overlap}')
     roof = None
     info = model.stage_info() if not args.no_timing else []
     if info:
@@ -141,9 +163,17 @@ def main():
                 'flops_per_launch': fl,
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
-        if name == 'persist':  # no progress callback -> one launch runs all S steps
+        if name == 'persist':  # no progress callback -> one launch per row batch runs all S steps
             S = model.fold_shape(args.frames, True, args.target, args.overlap)[1]
             roof['us_per_step'] = us / S
+            roof['launches_per_generate'] = n // max(args.steps, 1)
+        # HBM traffic of the same kernel on the same workload from the committed PMC passes
+        # (rocprofv3 cannot run inside this process; profiles/pmc_traffic.json names its source)
+        pmc = _pmc_traffic(kernel, workload)
+        if pmc:
+            roof['traffic'] = pmc['traffic_bytes']
+            roof['traffic_source'] = pmc['source']
+            roof['traffic_note'] = pmc['correction']
     result = {
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',
         'value': value, 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -152,9 +182,7 @@ def main():
         'data': 'synthetic (seeded random-init weights of the reference architecture, '
                 'uniform[-4,4] mels)',
         'xrtf': value / sp.sample_rate,
-        'config': {'workload': f'{U}x{args.frames}-frame mel per GPU, {args.model} {args.mode} '
-                               f'{args.bits}-bit mu-law, batched folds target={args.target} '
-                               f'overlap={args.overlap}',
+        'config': {'workload': workload,
                    'utts_per_gpu': U, 'frames': args.frames,
                    'fold_rows_per_gpu': U * model.fold_shape(args.frames, True, args.target,
                                                              args.overlap)[0],
