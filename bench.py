@@ -166,7 +166,7 @@ def main():
         if name == 'persist':  # no progress callback -> one launch per row batch runs all S steps
             S = model.fold_shape(args.frames, True, args.target, args.overlap)[1]
             roof['us_per_step'] = us / S
-            roof['launches_per_generate'] = n // max(args.steps, 1)
+            roof['launches_per_generate'] = n  # stage timing keeps the last generate's launches
         # HBM traffic of the same kernel on the same workload from the committed PMC passes
         # (rocprofv3 cannot run inside this process; profiles/pmc_traffic.json names its source)
         pmc = _pmc_traffic(kernel, workload)
