@@ -322,24 +322,34 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // waves 0-3 here, the rest by waves 4-7 in stage C (LDS weights, h2 staged in X1)
         auto hh2_rows = [&](int r0, int r1, int ul) {
             const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)ul * 3 * kPK4;
+            // weights read from LDS once per step, all of the rows accumulated per weight load
+            // (each accumulator sums in the same k order as a per-row loop would)
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            v2f acc[NR][3];
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[r][j] = (v2f){0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                float4 w4[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    if (r < r0 || r >= r1) continue;
+                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) dot4(acc[r][j], w4[j], x4);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 if (r < r0 || r >= r1) continue;
-                v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    float4 w4[3];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
-                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) dot4(acc[j], w4[j], x4);
-                }
-                const float t0 = row16_sum(hsum(acc[0]));
-                const float t1 = row16_sum(hsum(acc[1]));
-                const float t2 = row16_sum(hsum(acc[2]));
+                const float t0 = row16_sum(hsum(acc[r][0]));
+                const float t1 = row16_sum(hsum(acc[r][1]));
+                const float t2 = row16_sum(hsum(acc[r][2]));
                 if (kc == r) {
                     s0 = t0;
                     s1 = t1;
@@ -428,22 +438,27 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             float s0 = 0.f;
             if (has_cls) {
                 const float4* Wf = reinterpret_cast<const float4*>(lds + L_FC3) + (size_t)og * kPK4;
+                v2f acc[NR];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+#pragma unroll
+                for (int qb = 0; qb < 8; qb += 4) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    float4 wq[4];  // fc3 weights: one LDS read per step (10-bit: registers)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wq[q] = FC3R ? wr[(32 + qb + q) % NW] : Wf[16 * (qb + q) + kc];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        float4 xq[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) dot4(acc[r], wq[q], xq[q]);
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    v2f acc = {0.f, 0.f};
-#pragma unroll
-                    for (int qb = 0; qb < 8; qb += 4) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        float4 xq[4], wq[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
-                            wq[q] = FC3R ? wr[(32 + qb + q) % NW] : Wf[16 * (qb + q) + kc];
-                        }
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) dot4(acc, wq[q], xq[q]);
-                    }
-                    const float t0 = row16_sum(hsum(acc));
+                    const float t0 = row16_sum(hsum(acc[r]));
                     if (kc == r) s0 = t0;
                 }
             }
