@@ -8,7 +8,8 @@
  *   -----------------------------------------------------------  -------------------------------
  *   WaveRNNVocoder.Vocoder()        libwavernn/<variant>/src/     wrnn_create
  *                                   WaveRNNVocoder.cpp:17-21
- *   Vocoder.loadWeights(path)       WaveRNNVocoder.cpp:22-31       wrnn_load_tensor + wrnn_finalize
+ *   Vocoder.loadWeights(path)       WaveRNNVocoder.cpp:22-31       wrnn_load_bin (.bin image), or
+ *                                                                   wrnn_load_tensor + wrnn_finalize
  *   model.load_state_dict(sd)       vocoder/inference.py:35        (state-dict names, PyTorch layout)
  *   Vocoder.setRandomSeed(seed)     WaveRNNVocoder.cpp:33-35       wrnn_set_seed
  *   torch.manual_seed(seed)         vocoder/inference.py:97-101
@@ -56,8 +57,8 @@ extern "C" {
 
 /* Recurrence engines (same results, different schedules):
  *   CHAIN   one launch per layer group per step, HIP-graph captured (every topology)
- *   PERSIST one persistent weight-stationary launch per chunk of steps, 8 XCD-local groups
- *           (fatchord, rnn_dims = fc_dims = 512, <= 32 fold rows, n_classes <= 1024)
+ *   PERSIST one persistent weight-stationary launch per row batch, 8 XCD-local groups
+ *           (fatchord 512 / runtimeracer 256 dims, n_classes <= 1024, any row count)
  *   AUTO    PERSIST when the call qualifies, else CHAIN (default; env WRNN_ENGINE overrides) */
 #define WRNN_ENGINE_AUTO 0
 #define WRNN_ENGINE_CHAIN 1
@@ -103,6 +104,20 @@ int wrnn_load_tensor(wrnn_handle* h, const char* name, const float* data, const 
                      int ndim);
 /* Check every required tensor is present and repack them into the device layout. */
 int wrnn_finalize(wrnn_handle* h);
+
+/* libwavernn ".bin" weight files -- the second on-disk format of the reference, written by
+ * vocoder/libwavernn/convert.py:14-58 (dense or Pruner 1x4 block-compressed matrices) and read
+ * by Vocoder.loadWeights (WaveRNNVocoder.cpp:22-31, wavernn.cpp:37-184).
+ * wrnn_bin_read parses a whole file image (host memory) for the topology in `cfg` and hands
+ * every tensor to `fn` under its state-dict name, densified, in PyTorch layout; host only, no
+ * device is touched. A non-zero return of `fn` stops the read and is returned.
+ * wrnn_load_bin = wrnn_bin_read into wrnn_load_tensor, then wrnn_finalize. Format or shape
+ * mismatches are WRNN_ERR_INVALID ("libwavernn .bin: ..."). */
+typedef int (*wrnn_tensor_fn)(void* user, const char* name, const float* data,
+                              const int64_t* shape, int ndim);
+int wrnn_bin_read(const void* data, size_t bytes, const wrnn_config* cfg, wrnn_tensor_fn fn,
+                  void* user);
+int wrnn_load_bin(wrnn_handle* h, const void* data, size_t bytes);
 
 /* Seed of the Philox noise; resets the per-call stream counter (torch.manual_seed). */
 int wrnn_set_seed(wrnn_handle* h, uint64_t seed);

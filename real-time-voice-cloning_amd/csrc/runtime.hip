@@ -1540,8 +1540,6 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
     if (batched && (target <= 0 || overlap < 0))
         return fail(WRNN_ERR_INVALID, "target must be > 0 and overlap >= 0");
-    if (!batched && n_utts != 1)
-        return fail(WRNN_ERR_INVALID, "unbatched generation takes one utterance");
     std::vector<UttPlan> plan(n_utts);
     int B = 0, S = 0, P = 0, Fr = 0, Tmax = 0;
     for (int u = 0; u < n_utts; ++u) {
@@ -1552,7 +1550,9 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         int b, s;
         fold_shape(p.L, batched, target, overlap, &b, &s);
         if (b <= 0) return fail(WRNN_ERR_INVALID, "mel too short for target/overlap");
-        if (u && s != S) return fail(WRNN_ERR_INVALID, "inconsistent seq_len");
+        if (u && s != S)
+            return fail(WRNN_ERR_INVALID, batched ? "inconsistent seq_len"
+                                                  : "unbatched utterances of one call must have equal lengths");
         S = s;
         p.B = b;
         p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
@@ -1723,6 +1723,18 @@ int collect_timing(wrnn_handle* h) {
 extern "C" {
 
 const char* wrnn_version(void) { return "wavernn-mi355x 0.1 (gfx950)"; }
+
+int wrnn_internal_fail(int code, const char* msg) { return fail(code, msg ? msg : ""); }
+
+int wrnn_load_bin(wrnn_handle* h, const void* data, size_t bytes) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    auto put = [](void* u, const char* name, const float* d, const int64_t* shape, int ndim) -> int {
+        return wrnn_load_tensor(static_cast<wrnn_handle*>(u), name, d, shape, ndim);
+    };
+    const int rc = wrnn_bin_read(data, bytes, &h->cfg, put, h);
+    if (rc) return rc;
+    return wrnn_finalize(h);
+}
 
 const char* wrnn_last_error(void) { return g_err.c_str(); }
 

@@ -33,7 +33,7 @@ EXPORTED = [
     'wrnn_load_tensor', 'wrnn_finalize', 'wrnn_set_seed', 'wrnn_set_stream', 'wrnn_fold_shape',
     'wrnn_generate', 'wrnn_generate_batch_device', 'wrnn_enable_stage_timing',
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
-    'wrnn_set_engine', 'wrnn_last_engine',
+    'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
 ]
 
 
@@ -49,6 +49,10 @@ class WrnnConfig(ctypes.Structure):
 
 PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                ctypes.c_int, ctypes.c_double)
+
+TENSOR_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p,
+                             ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64),
+                             ctypes.c_int)
 
 _lib = None
 
@@ -87,6 +91,8 @@ def load_library(path=None):
         'wrnn_load_tensor': (c_int, [c_void_p, ctypes.c_char_p, P(ctypes.c_float),
                                      P(ctypes.c_int64), c_int]),
         'wrnn_finalize': (c_int, [c_void_p]),
+        'wrnn_bin_read': (c_int, [ctypes.c_char_p, c_size_t, P(WrnnConfig), TENSOR_FN, c_void_p]),
+        'wrnn_load_bin': (c_int, [c_void_p, ctypes.c_char_p, c_size_t]),
         'wrnn_set_seed': (c_int, [c_void_p, ctypes.c_uint64]),
         'wrnn_set_stream': (c_int, [c_void_p, ctypes.c_uint32]),
         'wrnn_fold_shape': (c_int, [c_int, c_int, c_int, c_int, c_int, P(c_int), P(c_int)]),

@@ -1,8 +1,9 @@
 """Model-type registry and factory (vocoder/models/base.py:8-120 of the reference).
 
 ``VOC_TYPE_MI355X`` is the backend added by this package; ``VOC_TYPE_PYTORCH`` is accepted as
-an alias so unmodified callers of ``load_model(path)`` land on the GPU path. The libwavernn
-``.bin`` format (``VOC_TYPE_CPP``) and the geneing topology are SURVEY.md §8f "next" items.
+an alias so unmodified callers of ``load_model(path)`` land on the GPU path; ``VOC_TYPE_CPP``
+('libwavernn') loads ``.bin`` files (wavernn_amd/libwavernn.py). The geneing topology is a
+SURVEY.md §8f "next" item.
 """
 import numpy as np
 

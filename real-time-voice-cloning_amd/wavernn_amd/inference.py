@@ -8,8 +8,9 @@ Same module-level singleton and the same four functions:
   progress_callback=None)``                                          (:59-95)
 * ``set_seed(seed)``                                                (:97-101)
 
-``voc_type`` 'pytorch' (the reference default) and 'mi355x' both select the GPU backend;
-'libwavernn' raises NotImplementedError (its .bin format is a SURVEY §8f next item).
+``voc_type`` 'pytorch' (the reference default) and 'mi355x' both select the GPU backend on a
+checkpoint; 'libwavernn' loads a ``.bin`` file (vocoder/libwavernn/convert.py) into the
+``wavernn_amd.libwavernn.Vocoder`` drop-in, as the reference does (:36-47, runtimeracer model).
 Checkpoints are read with ``torch.load(..., weights_only=True)``.
 """
 import os
@@ -32,11 +33,23 @@ def load_model(weights_fpath, voc_type=base.VOC_TYPE_PYTORCH, verbose=True, devi
     ``state_dict``/``model_type`` may be given directly instead of a path (tests, bench).
     """
     global _model, _model_type, _device
-    if voc_type not in (base.VOC_TYPE_PYTORCH, base.VOC_TYPE_MI355X):
+    if voc_type not in (base.VOC_TYPE_PYTORCH, base.VOC_TYPE_MI355X, base.VOC_TYPE_CPP):
         raise NotImplementedError("Invalid vocoder of type '%s' provided. Aborting..." % voc_type)
     if device is None:
         device = int(os.environ.get('LOCAL_RANK', 0))
     _device = device
+    if voc_type == base.VOC_TYPE_CPP:
+        from .libwavernn import Vocoder
+        # the reference hard-wires the runtimeracer topology here (vocoder/inference.py:38-39)
+        _model = Vocoder(weights_fpath, model_type or base.MODEL_TYPE_RUNTIMERACER, verbose,
+                         device=device)
+        if _seed is not None:
+            _model.setRandomSeed(_seed)
+        _model.load()
+        _model_type = voc_type
+        if verbose:
+            print("Loaded vocoder of model '%s' at path '%s'." % (_model_type, weights_fpath))
+        return
     if state_dict is None:
         import torch
         checkpoint = torch.load(weights_fpath, map_location='cpu', weights_only=True)
@@ -69,6 +82,8 @@ def infer_waveform(mel, normalize=True, batched=True, target=None, overlap=None,
     """Infers the waveform of a mel spectrogram output by the synthesizer."""
     if _model is None or _model_type is None:
         raise Exception("Please load Wave-RNN in memory before using it")
+    if _model_type == base.VOC_TYPE_CPP:
+        return _model.vocode_mel(mel=mel, normalize=normalize, progress_callback=progress_callback)
     hp_wavernn = base.hparams_for(_model_type)
     if target is None:
         target = hp_wavernn.gen_target
@@ -86,7 +101,10 @@ def set_seed(seed):
     global _seed
     _seed = seed
     if _model is not None:
-        _model.set_seed(seed)
+        if _model_type == base.VOC_TYPE_CPP:
+            _model.setRandomSeed(seed)
+        else:
+            _model.set_seed(seed)
 
 
 def get_model():

@@ -12,6 +12,7 @@ through the C-ABI; only the reference's f64 post-processing (cross-fade, mu-law,
 fade-out; fatchord_version.py:238-255) runs on the host, restated bit-exactly in audio.py.
 """
 import ctypes
+import os
 import sys
 import time
 
@@ -121,6 +122,18 @@ class WaveRNN:
                 self._h, name.encode(), arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                 shape, arr.ndim), 'load_state_dict')
         _abi.check(self._lib.wrnn_finalize(self._h), 'load_state_dict')
+        self._loaded = True
+
+    def load_bin(self, data):
+        """Load a libwavernn .bin weight file (path or bytes; vocoder/libwavernn/convert.py)."""
+        if isinstance(data, (str, os.PathLike)):
+            try:
+                with open(data, 'rb') as f:
+                    data = f.read()
+            except OSError:
+                raise RuntimeError("Cannot open file.")  # WaveRNNVocoder.cpp:24-26
+        data = bytes(data)
+        _abi.check(self._lib.wrnn_load_bin(self._h, data, len(data)), 'loadWeights')
         self._loaded = True
 
     def set_seed(self, seed):

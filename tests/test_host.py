@@ -68,6 +68,9 @@ def test_inference_api_surface():
     with pytest.raises(Exception, match='Please load Wave-RNN'):
         inference.infer_waveform(np.zeros((80, 10), np.float32))
     with pytest.raises(NotImplementedError):
-        inference.load_model('x.bin', voc_type='libwavernn')
+        inference.load_model('x.pt', voc_type='tensorflow')
+    import vocoder.libwavernn.inference as lw   # libwavernn drop-in (voc_type='libwavernn')
+    from wavernn_amd.libwavernn import Vocoder
+    assert lw.Vocoder is Vocoder
     import vocoder.inference as drop_in   # the reference's module name resolves to ours
     assert drop_in.infer_waveform is inference.infer_waveform
