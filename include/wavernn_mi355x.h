@@ -51,8 +51,9 @@ extern "C" {
 
 #define WRNN_MODEL_FATCHORD 0     /* 'fatchord-wavernn'     vocoder/models/base.py:13 */
 #define WRNN_MODEL_RUNTIMERACER 1 /* 'runtimeracer-wavernn' vocoder/models/base.py:15 */
+#define WRNN_MODEL_GENEING 2      /* 'geneing-wavernn'      vocoder/models/base.py:14 */
 
-#define WRNN_MODE_RAW 0 /* softmax over 2**bits classes, Categorical sample */
+#define WRNN_MODE_RAW 0 /* softmax over 2**bits classes, Categorical sample (geneing: 'BITS') */
 #define WRNN_MODE_MOL 1 /* 10-component discretized mixture of logistics   */
 
 /* Recurrence engines (same results, different schedules):

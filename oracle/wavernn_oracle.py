@@ -39,6 +39,7 @@ from oracle import philox
 
 MODEL_TYPE_FATCHORD = 'fatchord-wavernn'
 MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
+MODEL_TYPE_GENEING = 'geneing-wavernn'
 
 
 def _t(sd, name):
@@ -57,9 +58,13 @@ class OracleWaveRNN:
         self.model_type = model_type
         self.mode = hp.mode
         self.pad = hp.pad
-        self.n_classes = 2 ** hp.bits if hp.mode == 'RAW' else 30
+        if model_type == MODEL_TYPE_GENEING and hp.mode == 'RAW':
+            raise NotImplementedError('geneing RAW mode (Beta sampling) has no noise contract')
+        self.n_classes = 2 ** hp.bits if hp.mode in ('RAW', 'BITS') else 30
         self.rnn_dims = hp.rnn_dims
-        self.aux_dims = hp.res_out_dims // 4
+        # geneing_version.py:106 splits the aux into 2 parts, the others into 4
+        self.n_aux = 2 if model_type == MODEL_TYPE_GENEING else 4
+        self.aux_dims = hp.res_out_dims // self.n_aux
         self.hop_length = hop_length
         self.upsample_factors = tuple(hp.upsample_factors)
         self.indent = hp.pad * int(np.cumprod(self.upsample_factors)[-1])
@@ -166,6 +171,17 @@ class OracleWaveRNN:
         return F.linear(x, self.sd[name + '.weight'], self.sd[name + '.bias'])
 
     def step(self, x, hs, m_t, a_t):
+        if self.model_type == MODEL_TYPE_GENEING:  # geneing_version.py:193-205
+            a1_t, a2_t = a_t
+            x = torch.cat([x, m_t, a1_t[:, :-1]], dim=1)
+            x = self._lin('I', x)
+            h1, = hs
+            h1 = self._gru('rnn1', x, h1)
+            x = x + h1
+            x = torch.cat([x, a2_t], dim=1)
+            x = F.relu(self._lin('fc1', x))
+            logits = self._lin('fc3', x)
+            return logits, (h1,)
         a1_t, a2_t, a3_t, a4_t = a_t
         x = torch.cat([x, m_t, a1_t[:, :-1]], dim=1)
         x = self._lin('I', x)
@@ -251,7 +267,7 @@ class OracleWaveRNN:
         then None.
         ``record_logits``: optional list of step indices whose logits are returned.
         """
-        mu_law = mu_law if self.mode == 'RAW' else False
+        mu_law = mu_law if self.mode == 'RAW' else False  # geneing BITS: no mu-law (:158)
         start = time.time()
         out = {}
         with torch.no_grad():
@@ -260,11 +276,11 @@ class OracleWaveRNN:
             out['t_prepare'] = time.time() - t0
             b_size, seq_len, _ = mels.size()
             n_steps = seq_len if max_steps is None else min(seq_len, max_steps)
-            hs = tuple(torch.zeros(b_size, self.rnn_dims)
-                       for _ in range(2 if self.model_type == MODEL_TYPE_FATCHORD else 4))
+            n_gru = {MODEL_TYPE_FATCHORD: 2, MODEL_TYPE_GENEING: 1}.get(self.model_type, 4)
+            hs = tuple(torch.zeros(b_size, self.rnn_dims) for _ in range(n_gru))
             x = torch.zeros(b_size, 1)
             d = self.aux_dims
-            aux_split = [aux[:, :, d * i:d * (i + 1)] for i in range(4)]
+            aux_split = [aux[:, :, d * i:d * (i + 1)] for i in range(self.n_aux)]
             rows = np.arange(b_size)
             labels = np.zeros((b_size, n_steps), dtype=np.int16)
             samples = []
@@ -294,7 +310,7 @@ class OracleWaveRNN:
                     progress_callback(i, seq_len, b_size, gen_rate)
             out['t_loop'] = time.time() - t0
         out['B'], out['S'], out['steps'] = b_size, seq_len, n_steps
-        out['labels'] = labels if self.mode == 'RAW' else None
+        out['labels'] = labels if self.mode != 'MOL' else None
         output = torch.stack(samples).transpose(0, 1)
         out['samples'] = output.numpy().copy()
         out['logits'] = logits_rec

@@ -268,9 +268,13 @@ extern "C" int wrnn_bin_read(const void* data, size_t bytes, const wrnn_config* 
         E("upsample.up_layers." + std::to_string(2 * j + 1) + ".weight", r.floats(k), {1, 1, 1, k});
     }
     // main network (convert.py:327-351)
-    const int A = R / 4;
+    const int A = R / (cfg->model_type == WRNN_MODEL_GENEING ? 2 : 4);
     linear(r, E, "I", F0 + A, H);
-    if (cfg->model_type == WRNN_MODEL_FATCHORD) {
+    if (cfg->model_type == WRNN_MODEL_GENEING) {  // convert.py:336-340
+        gru(r, E, "rnn1", H, H);
+        linear(r, E, "fc1", H + A, Fc);
+        linear(r, E, "fc3", Fc, n);
+    } else if (cfg->model_type == WRNN_MODEL_FATCHORD) {
         gru(r, E, "rnn1", H, H);
         gru(r, E, "rnn2", H + A, H);
         linear(r, E, "fc1", H + A, Fc);

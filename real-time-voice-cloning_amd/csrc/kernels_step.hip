@@ -268,8 +268,11 @@ static hipError_t launch_stage_t(const StageArgs& a, int n_row_tiles, hipStream_
 
 template <int K, int RT>
 static hipError_t dispatch_nrg(bool prep, const StageArgs* a, int NRG, int nrt, hipStream_t s) {
-    switch (NRG) {
-        case 1: return prep ? prepare_stage_t<K, RT, 1>() : launch_stage_t<K, RT, 1>(*a, nrt, s);
+    switch (NRG) {  // K = 128 needs NRG >= 2 (4 k per thread; the runtime packs for that)
+        case 1:
+            if constexpr (K >= 256)
+                return prep ? prepare_stage_t<K, RT, 1>() : launch_stage_t<K, RT, 1>(*a, nrt, s);
+            return hipErrorInvalidValue;
         case 2: return prep ? prepare_stage_t<K, RT, 2>() : launch_stage_t<K, RT, 2>(*a, nrt, s);
         case 4: return prep ? prepare_stage_t<K, RT, 4>() : launch_stage_t<K, RT, 4>(*a, nrt, s);
         default: return hipErrorInvalidValue;
@@ -294,6 +297,7 @@ static hipError_t dispatch_rt(bool prep, const StageArgs* a, int RT, int NRG, in
 hipError_t prepare_stage(int K, int RT, int NRG) {
     if (K == 512) return dispatch_rt<512>(true, nullptr, RT, NRG, 0, nullptr);
     if (K == 256) return dispatch_rt<256>(true, nullptr, RT, NRG, 0, nullptr);
+    if (K == 128) return dispatch_rt<128>(true, nullptr, RT, NRG, 0, nullptr);
     return hipErrorInvalidValue;
 }
 
@@ -301,6 +305,7 @@ hipError_t launch_stage(const StageArgs& a, int K, int RT, int NRG, int n_row_ti
                         hipStream_t s) {
     if (K == 512) return dispatch_rt<512>(false, &a, RT, NRG, n_row_tiles, s);
     if (K == 256) return dispatch_rt<256>(false, &a, RT, NRG, n_row_tiles, s);
+    if (K == 128) return dispatch_rt<128>(false, &a, RT, NRG, n_row_tiles, s);
     return hipErrorInvalidValue;
 }
 

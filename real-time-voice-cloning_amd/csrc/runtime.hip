@@ -255,6 +255,10 @@ void build_expected(wrnn_handle* h) {
         lin("fc1", H + A, F);
         lin("fc2", F + A, F);
         lin("fc3", F, n);
+    } else if (h->cfg.model_type == WRNN_MODEL_GENEING) {  // geneing_version.py:111-114
+        gru("rnn1", H);
+        lin("fc1", H + A, F);
+        lin("fc3", F, n);
     } else {
         gru("rnn1", H);
         gru("rnn2", H);
@@ -631,9 +635,13 @@ int do_finalize(wrnn_handle* h) {
         return ac.offset;
     };
     const int K = H;  // recurrent inner dimension
-    if (H != F) return fail(WRNN_ERR_INVALID, "rnn_dims != fc_dims is not supported");
+    const bool geneing = h->cfg.model_type == WRNN_MODEL_GENEING;
+    if (!geneing && H != F) return fail(WRNN_ERR_INVALID, "rnn_dims != fc_dims is not supported");
     if (K != 256 && K != 512)
         return fail(WRNN_ERR_INVALID, "rnn_dims must be 256 or 512 (got " + std::to_string(K) + ")");
+    if (geneing && F != 128 && F != 256 && F != 512)
+        return fail(WRNN_ERR_INVALID, "fc_dims must be 128, 256 or 512 (got " + std::to_string(F) + ")");
+    if (F < 256 && h->nrg < 2) h->nrg = 2;  // K = 128 tiles need >= 4 k per thread
     if (h->cfg.mode == WRNN_MODE_RAW && n % 4)
         return fail(WRNN_ERR_INVALID, "n_classes must be a multiple of 4");
     auto seg_gru = [&](const std::string& gname, int col0_ld, int x, int gh, int hh, int xout,
@@ -676,9 +684,9 @@ int do_finalize(wrnn_handle* h) {
         return s;
     };
     auto seg_fc = [&](const std::string& nm, int n_out, int ld, int x, int y, bool relu,
-                      const float* cond, int fc) {
+                      const float* cond, int fc, int Kin = 0) {
         SegDesc s{};
-        s.w = pack_segment(h, T[nm + ".weight"], n_out, ld, 0, K, TILE_OUT, 0, &rc);
+        s.w = pack_segment(h, T[nm + ".weight"], n_out, ld, 0, Kin ? Kin : K, TILE_OUT, 0, &rc);
         s.kind = relu ? EPI_COND_RELU : EPI_COND;
         s.x = x;
         s.y = y;
@@ -709,6 +717,23 @@ int do_finalize(wrnn_handle* h) {
         CHECK(rc);
         h->stages = {s0, s1, s2, s3};
         CHECK(pack_persist(h, oG2, oF1, oF2));
+    } else if (geneing) {
+        // geneing_version.py:193-205: x1 = I(x0) + rnn1(...) ; y1 = relu(fc1([x1, a2])) ;
+        // logits = fc3(y1). Stage 0 (K = H): fc1, W_hh1 h1, P1 of the next step; stage 1
+        // (K = F): fc3. GRU1 runs in the sampler.
+        h->pw.ok = false;
+        h->pw.rr = false;
+        const int oF1 = add_aux(1, "fc1.weight", "fc1.bias", F, H + A, H);
+        CHECK(rc);
+        h->cond_width = off;
+        StageDesc s0{"fc1", K, {}, true};
+        s0.segs.push_back(seg_fc("fc1", F, H + A, SL_X1, SL_Y1, true, nullptr, fcol(oF1)));
+        s0.segs.push_back(seg_hh("rnn1", SL_H1, SL_GH1));
+        s0.segs.push_back(seg_p1());
+        StageDesc s1{"fc3", F, {}, false};
+        s1.segs.push_back(seg_fc("fc3", n, F, SL_Y1, SL_LOG, false, dv("fc3.bias"), -1, F));
+        CHECK(rc);
+        h->stages = {s0, s1};
     } else {
         h->pw.ok = false;
         h->pw.rr = false;
@@ -1168,7 +1193,7 @@ int run_chain(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     auto& ws = h->ws;
     const int B = h->last_B;
     h->RT = pick_rt(B, &h->nrt);
-    HIPC(prepare_stage(h->stages[0].K, h->RT, h->nrg));
+    for (const StageDesc& sd : h->stages) HIPC(prepare_stage(sd.K, h->RT, h->nrg));
     {
         const char* env = std::getenv("WRNN_PHASE_STEP");
         h->phase_step = env ? std::atoi(env) : -1;
@@ -1222,7 +1247,7 @@ int run_chain(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         sa.rows = (const RowInfo*)ws.rows.p;
         HIPC(launch_sample(sa, h->stream));
     }
-    HIPC(prepare_stage(h->stages[0].K, h->RT, h->nrg));
+    for (const StageDesc& sd : h->stages) HIPC(prepare_stage(sd.K, h->RT, h->nrg));
     if (h->timing) {
         const size_t need = ((size_t)S / kStampEvery + 1) * h->stages.size() * kMaxStampWG * 2 *
                             sizeof(uint32_t);
@@ -1747,7 +1772,8 @@ int wrnn_device_count(int* count) {
 int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
     if (!cfg || !out) return fail(WRNN_ERR_INVALID, "null argument");
     *out = nullptr;
-    if (cfg->model_type != WRNN_MODEL_FATCHORD && cfg->model_type != WRNN_MODEL_RUNTIMERACER)
+    if (cfg->model_type != WRNN_MODEL_FATCHORD && cfg->model_type != WRNN_MODEL_RUNTIMERACER &&
+        cfg->model_type != WRNN_MODEL_GENEING)
         return fail(WRNN_ERR_INVALID, "Invalid model type " + std::to_string(cfg->model_type));
     if (cfg->mode != WRNN_MODE_RAW && cfg->mode != WRNN_MODE_MOL)
         return fail(WRNN_ERR_INVALID, "Unknown model mode value - " + std::to_string(cfg->mode));
@@ -1759,20 +1785,22 @@ int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
     for (int i = 0; i < cfg->n_upsample; ++i) prod *= cfg->upsample_factors[i];
     if (prod != cfg->hop_length)
         return fail(WRNN_ERR_INVALID, "prod(upsample_factors) != hop_length");  // base.py:27
-    if (cfg->res_out_dims % 4 || cfg->res_out_dims / 4 < 2)
-        return fail(WRNN_ERR_INVALID, "res_out_dims must be a multiple of 4");
+    // aux split: 4 parts (fatchord, runtimeracer), 2 parts (geneing_version.py:106)
+    const int n_aux = cfg->model_type == WRNN_MODEL_GENEING ? 2 : 4;
+    if (cfg->res_out_dims % n_aux || cfg->res_out_dims / n_aux < 2)
+        return fail(WRNN_ERR_INVALID, "res_out_dims must be a multiple of " + std::to_string(n_aux));
     std::unique_ptr<wrnn_handle> h(new wrnn_handle());
     h->cfg = *cfg;
     h->device = device;
     h->H = cfg->rnn_dims;
     h->F = cfg->fc_dims;
-    h->A = cfg->res_out_dims / 4;
+    h->A = cfg->res_out_dims / n_aux;
     h->C = cfg->compute_dims;
     h->R = cfg->res_out_dims;
     h->feat = cfg->feat_dims;
     h->hop = cfg->hop_length;
     h->n_classes = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : 30;
-    h->n_gru = cfg->model_type == WRNN_MODEL_FATCHORD ? 2 : 4;
+    h->n_gru = cfg->model_type == WRNN_MODEL_FATCHORD ? 2 : cfg->model_type == WRNN_MODEL_GENEING ? 1 : 4;
     h->indent = cfg->pad * prod;
     build_expected(h.get());
     HIPC(hipSetDevice(device));

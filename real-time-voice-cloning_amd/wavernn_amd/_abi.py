@@ -20,6 +20,7 @@ WRNN_ERR_CAPACITY = -6
 
 WRNN_MODEL_FATCHORD = 0
 WRNN_MODEL_RUNTIMERACER = 1
+WRNN_MODEL_GENEING = 2
 WRNN_MODE_RAW = 0
 WRNN_MODE_MOL = 1
 

@@ -2,19 +2,18 @@
 
 ``VOC_TYPE_MI355X`` is the backend added by this package; ``VOC_TYPE_PYTORCH`` is accepted as
 an alias so unmodified callers of ``load_model(path)`` land on the GPU path; ``VOC_TYPE_CPP``
-('libwavernn') loads ``.bin`` files (wavernn_amd/libwavernn.py). The geneing topology is a
-SURVEY.md §8f "next" item.
+('libwavernn') loads ``.bin`` files (wavernn_amd/libwavernn.py). All three registered model
+types are built: fatchord, runtimeracer and geneing (modes BITS and MOL; its Beta 'RAW' mode
+raises NotImplementedError).
 """
 import numpy as np
 
-from .hparams import sp, wavernn_fatchord, wavernn_runtimeracer
-from .model import WaveRNN, MODEL_TYPE_FATCHORD, MODEL_TYPE_RUNTIMERACER
+from .hparams import sp, wavernn_fatchord, wavernn_geneing, wavernn_runtimeracer
+from .model import WaveRNN, MODEL_TYPE_FATCHORD, MODEL_TYPE_GENEING, MODEL_TYPE_RUNTIMERACER
 
 VOC_TYPE_CPP = 'libwavernn'
 VOC_TYPE_PYTORCH = 'pytorch'
 VOC_TYPE_MI355X = 'mi355x'
-
-MODEL_TYPE_GENEING = 'geneing-wavernn'
 
 
 def hparams_for(model_type):
@@ -22,6 +21,8 @@ def hparams_for(model_type):
         return wavernn_fatchord
     if model_type == MODEL_TYPE_RUNTIMERACER:
         return wavernn_runtimeracer
+    if model_type == MODEL_TYPE_GENEING:
+        return wavernn_geneing
     raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
 
 
@@ -32,6 +33,8 @@ def init_voc_model(model_type, device, override_hp_fatchord=None, override_hp_ge
         hparams = override_hp_fatchord or wavernn_fatchord
     elif model_type == MODEL_TYPE_RUNTIMERACER:
         hparams = override_hp_runtimeracer or wavernn_runtimeracer
+    elif model_type == MODEL_TYPE_GENEING:
+        hparams = override_hp_geneing or wavernn_geneing
     else:
         raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
     assert np.cumprod(hparams.upsample_factors)[-1] == sp.hop_size

@@ -105,7 +105,7 @@ class _Writer:
 
 def write_bin(f, state_dict, hp, model_type):
     """Write ``state_dict`` of a ``model_type`` WaveRNN with hparams ``hp`` as a .bin stream."""
-    from .model import MODEL_TYPE_FATCHORD, MODEL_TYPE_RUNTIMERACER
+    from .model import MODEL_TYPE_FATCHORD, MODEL_TYPE_GENEING, MODEL_TYPE_RUNTIMERACER
     sd = state_dict
     w = _Writer(f)
     scale = int(np.prod(hp.upsample_factors))
@@ -130,6 +130,8 @@ def write_bin(f, state_dict, hp, model_type):
     w.linear(sd, 'I')
     if model_type == MODEL_TYPE_FATCHORD:
         grus, fcs = ('rnn1', 'rnn2'), ('fc1', 'fc2', 'fc3')
+    elif model_type == MODEL_TYPE_GENEING:  # convert.py:336-340
+        grus, fcs = ('rnn1',), ('fc1', 'fc3')
     elif model_type == MODEL_TYPE_RUNTIMERACER:
         grus, fcs = ('rnn1', 'rnn2', 'rnn3', 'rnn4'), ('fc1', 'fc2', 'fc3', 'fc4', 'fc5')
     else:
@@ -158,7 +160,7 @@ def config_for(hp, model_type):
     from .model import _MODEL_IDS
     cfg = _abi.WrnnConfig()
     cfg.model_type = _MODEL_IDS[model_type]
-    cfg.mode = _abi.WRNN_MODE_RAW if hp.mode == 'RAW' else _abi.WRNN_MODE_MOL
+    cfg.mode = _abi.WRNN_MODE_MOL if hp.mode == 'MOL' else _abi.WRNN_MODE_RAW
     cfg.bits = hp.bits
     cfg.rnn_dims, cfg.fc_dims = hp.rnn_dims, hp.fc_dims
     cfg.compute_dims, cfg.res_out_dims = hp.compute_dims, hp.res_out_dims

@@ -2,8 +2,8 @@
 
 Mirrors ``config/hparams.py`` of the reference: the ``HParams`` container (:7-29, including
 the comma-separated ``parse`` override), the signal-processing block ``sp`` (:38-51) and the
-two WaveRNN topologies this build runs, ``wavernn_fatchord`` (:220-285) and
-``wavernn_runtimeracer`` (:356-421). Only the fields the inference path reads are kept;
+three WaveRNN topologies this build runs, ``wavernn_fatchord`` (:220-285),
+``wavernn_geneing`` (:288-354) and ``wavernn_runtimeracer`` (:356-421). Only the fields the inference path reads are kept;
 training-schedule, pruning and anomaly-detection fields are out of scope.
 """
 import ast
@@ -90,4 +90,21 @@ wavernn_runtimeracer = HParams(
     gen_batched=True,
     gen_target=6000,
     gen_overlap=1000,
+)
+
+# config/hparams.py:288-354 (inference fields); mode 'BITS' = softmax over 2**bits classes
+wavernn_geneing = HParams(
+    mode='BITS',
+    bits=10,
+    mu_law=False,
+    upsample_factors=(4, 5, 10),
+    rnn_dims=256,
+    fc_dims=128,
+    compute_dims=64,
+    res_out_dims=32 * 2,
+    res_blocks=3,
+    pad=2,
+    gen_batched=True,
+    gen_target=3000,
+    gen_overlap=1500,
 )

@@ -23,8 +23,10 @@ from .audio import labels_to_samples, postprocess
 
 MODEL_TYPE_FATCHORD = 'fatchord-wavernn'
 MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
+MODEL_TYPE_GENEING = 'geneing-wavernn'
 _MODEL_IDS = {MODEL_TYPE_FATCHORD: _abi.WRNN_MODEL_FATCHORD,
-              MODEL_TYPE_RUNTIMERACER: _abi.WRNN_MODEL_RUNTIMERACER}
+              MODEL_TYPE_RUNTIMERACER: _abi.WRNN_MODEL_RUNTIMERACER,
+              MODEL_TYPE_GENEING: _abi.WRNN_MODEL_GENEING}
 
 
 def _progbar(i, n, size=16):
@@ -42,20 +44,28 @@ class WaveRNN:
     def __init__(self, rnn_dims, fc_dims, bits, pad, upsample_factors, feat_dims, compute_dims,
                  res_out_dims, res_blocks, hop_length, sample_rate, mode='RAW', pruning=False,
                  model_type=MODEL_TYPE_FATCHORD, device=0):
-        if mode == 'RAW':
+        if model_type not in _MODEL_IDS:
+            raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
+        geneing = model_type == MODEL_TYPE_GENEING
+        if geneing and mode == 'RAW':
+            # geneing_version.py:95-96,207-210: RAW = 2 Beta parameters; torch's Beta sampler
+            # (rejection-sampled gammas) has no noise contract here
+            raise NotImplementedError("geneing-wavernn mode 'RAW' (Beta sampling) is not supported; "
+                                      "use 'BITS' or 'MOL'")
+        if mode == 'RAW' or (geneing and mode == 'BITS'):
             self.n_classes = 2 ** bits
         elif mode == 'MOL':
             self.n_classes = 30
         else:
             raise RuntimeError("Unknown model mode value - ", mode)
-        if model_type not in _MODEL_IDS:
-            raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
+        # categorical sampling over n_classes: RAW (fatchord / runtimeracer) and geneing BITS
+        self.categorical = mode != 'MOL'
         self.mode = mode
         self.bits = bits
         self.pad = pad
         self.rnn_dims = rnn_dims
         self.fc_dims = fc_dims
-        self.aux_dims = res_out_dims // 4
+        self.aux_dims = res_out_dims // (2 if geneing else 4)
         self.hop_length = hop_length
         self.sample_rate = sample_rate
         self.model_type = model_type
@@ -65,7 +75,7 @@ class WaveRNN:
         self._lib = _abi.load_library()
         cfg = _abi.WrnnConfig()
         cfg.model_type = _MODEL_IDS[model_type]
-        cfg.mode = _abi.WRNN_MODE_RAW if mode == 'RAW' else _abi.WRNN_MODE_MOL
+        cfg.mode = _abi.WRNN_MODE_RAW if self.categorical else _abi.WRNN_MODE_MOL
         cfg.bits = bits
         cfg.rnn_dims, cfg.fc_dims = rnn_dims, fc_dims
         cfg.compute_dims, cfg.res_out_dims = compute_dims, res_out_dims
@@ -217,8 +227,8 @@ class WaveRNN:
         T = mel.shape[-1]
         B, S = self.fold_shape(T, batched, target, overlap)
         n = B * S
-        labels = np.empty((B, S), dtype=np.int16) if self.mode == 'RAW' else None
-        samples = None if self.mode == 'RAW' else np.empty((B, S), dtype=np.float32)
+        labels = np.empty((B, S), dtype=np.int16) if self.categorical else None
+        samples = None if self.categorical else np.empty((B, S), dtype=np.float32)
         cb_ref = [None]
 
         if progress_callback is not None:
@@ -269,7 +279,7 @@ class WaveRNN:
             b, S = self.fold_shape(int(m.shape[-1]), batched, target, overlap)
             rows += b
         dev = mels_dev[0].device
-        if self.mode == 'RAW':
+        if self.categorical:
             out = torch.empty((rows, S), dtype=torch.int16, device=dev)
             lab_p, smp_p = out.data_ptr(), None
         else:
@@ -297,7 +307,7 @@ class WaveRNN:
         wavs = []
         for u, m in enumerate(mels_dev):
             rows = host[roff[u]:roff[u + 1]]
-            smp = labels_to_samples(rows, self.n_classes) if self.mode == 'RAW' else rows
+            smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
             wave_len = (int(m.shape[-1]) - 1) * self.hop_length
             wavs.append(postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
                                     self.n_classes, wave_len, self.hop_length))

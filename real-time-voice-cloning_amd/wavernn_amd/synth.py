@@ -6,8 +6,8 @@ generator is numpy PCG64 so any machine (this container or a GPU box without the
 reference) regenerates bit-identical tensors from a seed.
 
 Key names and shapes follow the reference modules:
-``vocoder/models/fatchord_version.py:9-118`` and ``vocoder/models/runtimeracer_version.py``
-``:98-137`` (``upsample.resnet.*``, ``upsample.up_layers.{1,3,5}.weight``, ``I``, ``rnn*``,
+``vocoder/models/fatchord_version.py:9-118``, ``vocoder/models/geneing_version.py:88-120`` and
+``vocoder/models/runtimeracer_version.py:98-137`` (``upsample.resnet.*``, ``upsample.up_layers.{1,3,5}.weight``, ``I``, ``rnn*``,
 ``fc*``, ``step``). Init ranges follow torch's defaults for those module types
 (U(+-1/sqrt(fan_in)) for Linear/Conv, U(+-1/sqrt(hidden)) for GRU); BatchNorm statistics are
 randomised so that folding and ordering bugs cannot hide behind the identity transform.
@@ -16,10 +16,16 @@ import numpy as np
 
 MODEL_TYPE_FATCHORD = 'fatchord-wavernn'
 MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
+MODEL_TYPE_GENEING = 'geneing-wavernn'
 
 
 def n_classes_of(hp):
-    return 2 ** hp.bits if hp.mode == 'RAW' else 30
+    return 2 ** hp.bits if hp.mode in ('RAW', 'BITS') else 30
+
+
+def aux_dims_of(hp, model_type):
+    """res_out_dims // 4 (fatchord, runtimeracer) or // 2 (geneing_version.py:106)."""
+    return hp.res_out_dims // (2 if model_type == MODEL_TYPE_GENEING else 4)
 
 
 def state_dict_spec(hp, model_type, feat_dims=80):
@@ -43,7 +49,7 @@ def state_dict_spec(hp, model_type, feat_dims=80):
     for j, s in enumerate(hp.upsample_factors):
         spec[f'upsample.up_layers.{2 * j + 1}.weight'] = (1, 1, 1, 2 * s + 1)
     H, F = hp.rnn_dims, hp.fc_dims
-    A = R // 4
+    A = aux_dims_of(hp, model_type)
     n = n_classes_of(hp)
     spec['I.weight'] = (H, feat_dims + A)
     spec['I.bias'] = (H,)
@@ -63,6 +69,10 @@ def state_dict_spec(hp, model_type, feat_dims=80):
         gru('rnn2', H + A)
         lin('fc1', H + A, F)
         lin('fc2', F + A, F)
+        lin('fc3', F, n)
+    elif model_type == MODEL_TYPE_GENEING:
+        gru('rnn1', H)
+        lin('fc1', H + A, F)
         lin('fc3', F, n)
     elif model_type == MODEL_TYPE_RUNTIMERACER:
         gru('rnn1', H)
@@ -116,7 +126,7 @@ def synth_state_dict(hp, model_type, seed=0, logit_scale=1.0, feat_dims=80):
             b = 1.0 / np.sqrt(fan)
             w = rng.uniform(-b, b, size=shape)
         sd[name] = np.ascontiguousarray(w, dtype=np.float32)
-    last_fc = 'fc3' if model_type == MODEL_TYPE_FATCHORD else 'fc5'
+    last_fc = 'fc5' if model_type == MODEL_TYPE_RUNTIMERACER else 'fc3'
     if logit_scale != 1.0:
         sd[f'{last_fc}.weight'] = (sd[f'{last_fc}.weight'] * np.float32(logit_scale)).astype(np.float32)
         sd[f'{last_fc}.bias'] = (sd[f'{last_fc}.bias'] * np.float32(logit_scale)).astype(np.float32)

@@ -28,8 +28,9 @@ def golden_case(name):
 
 
 def hparams_of(meta):
-    from wavernn_amd.hparams import wavernn_fatchord, wavernn_runtimeracer
-    base = wavernn_fatchord if meta['model_type'] == 'fatchord-wavernn' else wavernn_runtimeracer
+    from wavernn_amd.hparams import wavernn_fatchord, wavernn_geneing, wavernn_runtimeracer
+    base = {'fatchord-wavernn': wavernn_fatchord, 'geneing-wavernn': wavernn_geneing,
+            'runtimeracer-wavernn': wavernn_runtimeracer}[meta['model_type']]
     return base.copy(bits=meta['bits'], mode=meta['mode'])
 
 

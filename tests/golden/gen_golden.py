@@ -52,6 +52,13 @@ CASES = {
                                 107, [0]),
     'runtimeracer_raw10_defaults': ('runtimeracer-wavernn', 'RAW', 10, 71, True, None, None, 8,
                                     18, 1.0, 108, [0]),
+    # geneing topology: 'BITS' = softmax over 2**bits classes, no mu-law
+    'geneing_bits10_tiny': ('geneing-wavernn', 'BITS', 10, 24, True, 1000, 100, 9, 19, 1.0, 109,
+                            [0, 1, 900]),
+    'geneing_mol_tiny': ('geneing-wavernn', 'MOL', 10, 24, True, 1000, 100, 10, 20, 1.0, 110,
+                         [0, 2]),
+    'geneing_bits9_defaults': ('geneing-wavernn', 'BITS', 9, 53, True, None, None, 11, 21, 1.0,
+                               111, [0]),
     # BASELINE.json configs[0]: 200-frame random mel, mu-law 9-bit, target=11000 overlap=550
     'fatchord_raw9_config1': ('fatchord-wavernn', 'RAW', 9, 200, True, 11000, 550, 0, 0, 1.0, 0,
                               [0, 1, 6000, 12099]),
@@ -142,7 +149,8 @@ def make_mol_patch(orig):
 def ref_hparams(model_type, mode, bits):
     from config import hparams as H
     import copy
-    base = H.wavernn_fatchord if model_type == 'fatchord-wavernn' else H.wavernn_runtimeracer
+    base = {'fatchord-wavernn': H.wavernn_fatchord, 'geneing-wavernn': H.wavernn_geneing,
+            'runtimeracer-wavernn': H.wavernn_runtimeracer}[model_type]
     hp = copy.deepcopy(base)
     hp.mode = mode
     hp.bits = bits
@@ -156,11 +164,14 @@ def run_reference(name, case):
     from vocoder.models import base
     import vocoder.models.fatchord_version as fv
     import vocoder.models.runtimeracer_version as rv
+    import vocoder.models.geneing_version as gv
     import vocoder.inference as vinf
 
     hp = ref_hparams(model_type, mode, bits)
     if model_type == 'fatchord-wavernn':
         model, _ = base.init_voc_model(model_type, torch.device('cpu'), override_hp_fatchord=hp)
+    elif model_type == 'geneing-wavernn':
+        model, _ = base.init_voc_model(model_type, torch.device('cpu'), override_hp_geneing=hp)
     else:
         model, _ = base.init_voc_model(model_type, torch.device('cpu'),
                                        override_hp_runtimeracer=hp)
@@ -181,10 +192,11 @@ def run_reference(name, case):
     # vocoder.inference singletons (inference.py:7-8) -> drive infer_waveform itself
     vinf._model = model
     vinf._model_type = model_type
-    hp_name = 'wavernn_fatchord' if model_type == 'fatchord-wavernn' else 'wavernn_runtimeracer'
+    hp_name = {'fatchord-wavernn': 'wavernn_fatchord', 'geneing-wavernn': 'wavernn_geneing',
+               'runtimeracer-wavernn': 'wavernn_runtimeracer'}[model_type]
     setattr(vinf, hp_name, hp)
 
-    last_fc = model.fc3 if model_type == 'fatchord-wavernn' else model.fc5
+    last_fc = model.fc5 if model_type == 'runtimeracer-wavernn' else model.fc3
     rec = {}
 
     def hook(mod, inp, out):
@@ -197,8 +209,10 @@ def run_reference(name, case):
     real_cat = torch.distributions.Categorical
     torch.distributions.Categorical = PatchedCategorical
     fv_orig, rv_orig = fv.sample_from_discretized_mix_logistic, rv.sample_from_discretized_mix_logistic
+    gv_orig = gv.sample_from_discretized_mix_logistic
     fv.sample_from_discretized_mix_logistic = make_mol_patch(fv_orig)
     rv.sample_from_discretized_mix_logistic = make_mol_patch(rv_orig)
+    gv.sample_from_discretized_mix_logistic = make_mol_patch(gv_orig)
     captured = {}
     orig_stack = torch.stack
 
@@ -217,13 +231,14 @@ def run_reference(name, case):
         torch.distributions.Categorical = real_cat
         fv.sample_from_discretized_mix_logistic = fv_orig
         rv.sample_from_discretized_mix_logistic = rv_orig
+        gv.sample_from_discretized_mix_logistic = gv_orig
         hnd.remove()
     dt = time.time() - t0
     model.eval()
     samples = captured['samples']
     res = dict(wav=np.asarray(wav, dtype=np.float64), samples=samples.astype(np.float32),
                steps=NoiseState.step, t=dt)
-    if mode == 'RAW':
+    if mode != 'MOL':
         n = 2 ** bits
         # labels recovered exactly from the fp32 samples: sample = 2k/(n-1) - 1 (fp32)
         ks = np.arange(n, dtype=np.float32)
@@ -263,7 +278,7 @@ def main():
         t_or = time.time() - t0
         same_wav = np.array_equal(o['wav'], res['wav'])
         same_samples = np.array_equal(o['samples'], res['samples'])
-        same_labels = (mode != 'RAW') or np.array_equal(o['labels'], res['labels'])
+        same_labels = (mode == 'MOL') or np.array_equal(o['labels'], res['labels'])
         same_logits = all(np.array_equal(o['logits'][s], res['logits'][s]) for s in rec_steps)
         print(f"{name}: B={o['B']} S={o['S']} ref {res['t']:.1f}s oracle {t_or:.1f}s "
               f"wav_eq={same_wav} samples_eq={same_samples} labels_eq={same_labels} "
@@ -271,7 +286,7 @@ def main():
         assert same_wav and same_samples and same_labels and same_logits, name
         out = dict(wav=res['wav'], logits_steps=np.array(rec_steps, dtype=np.int64),
                    logits=np.stack([res['logits'][s] for s in rec_steps]).astype(np.float32))
-        if mode == 'RAW':
+        if mode != 'MOL':
             out['labels'] = res['labels']
         else:
             out['samples'] = res['samples']

@@ -19,18 +19,20 @@ pytestmark = pytest.mark.gpu
 def _model(hp, mt):
     from wavernn_amd.base import init_voc_model
     from wavernn_amd.hparams import sp  # noqa: F401
-    m, _ = init_voc_model(mt, 0, override_hp_fatchord=hp, override_hp_runtimeracer=hp)
+    m, _ = init_voc_model(mt, 0, override_hp_fatchord=hp, override_hp_runtimeracer=hp,
+                          override_hp_geneing=hp)
     return m
 
 
-@pytest.mark.parametrize('mt,bits', [('fatchord-wavernn', 9), ('runtimeracer-wavernn', 10)])
+@pytest.mark.parametrize('mt,bits', [('fatchord-wavernn', 9), ('runtimeracer-wavernn', 10),
+                                     ('geneing-wavernn', 10)])
 @pytest.mark.parametrize('keep', [1.0, 0.3])
 def test_bin_loaded_model_equals_state_dict_model(mt, bits, keep):
     from wavernn_amd import convert
     from wavernn_amd.base import hparams_for
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    hp = hparams_for(mt).copy(bits=bits, mode='RAW')
+    hp = hparams_for(mt).copy(bits=bits)
     sd = pruned_state_dict(hp, mt, keep=keep)
     f = io.BytesIO()
     convert.write_bin(f, sd, hp, mt)

@@ -47,19 +47,20 @@ def first_divergence(a, b):
     return None if len(d) == 0 else tuple(d[np.argmin(d[:, 1])])
 
 
-def engine_cases(mode):
-    # both engines run both topologies (PERSIST: kernels_persist.hip for fatchord,
-    # kernels_persist_rr.hip for runtimeracer)
+def engine_cases(*modes):
+    # CHAIN runs every topology; PERSIST runs fatchord (kernels_persist.hip) and runtimeracer
+    # (kernels_persist_rr.hip)
     out = []
     for k, v in golden_meta().items():
-        if v['mode'] != mode:
+        if v['mode'] not in modes:
             continue
         out.append((k, 'chain'))
-        out.append((k, 'persist'))
+        if v['model_type'] != 'geneing-wavernn':
+            out.append((k, 'persist'))
     return out
 
 
-RAW_CASES = engine_cases('RAW')
+RAW_CASES = engine_cases('RAW', 'BITS')  # geneing 'BITS' = categorical over 2**bits classes
 MOL_CASES = engine_cases('MOL')
 
 

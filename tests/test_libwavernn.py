@@ -32,7 +32,7 @@ def pruned_state_dict(hp, model_type, seed=3, keep=0.5):
     return sd
 
 
-TOPOLOGIES = [('fatchord-wavernn', 9), ('runtimeracer-wavernn', 10)]
+TOPOLOGIES = [('fatchord-wavernn', 9), ('runtimeracer-wavernn', 10), ('geneing-wavernn', 10)]
 
 
 @pytest.mark.parametrize('model_type,bits', TOPOLOGIES)
@@ -40,7 +40,7 @@ TOPOLOGIES = [('fatchord-wavernn', 9), ('runtimeracer-wavernn', 10)]
 def test_bin_round_trip(model_type, bits, keep):
     from wavernn_amd import convert
     from wavernn_amd.base import hparams_for
-    hp = hparams_for(model_type).copy(bits=bits, mode='RAW')
+    hp = hparams_for(model_type).copy(bits=bits)
     sd = pruned_state_dict(hp, model_type, keep=keep)
     f = io.BytesIO()
     convert.write_bin(f, sd, hp, model_type)

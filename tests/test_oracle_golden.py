@@ -28,7 +28,7 @@ def run_oracle(name):
 def check(name):
     meta, gold, o = run_oracle(name)
     assert (o['B'], o['S']) == (meta['num_folds'], meta['seq_len'])
-    if meta['mode'] == 'RAW':
+    if meta['mode'] != 'MOL':  # RAW / geneing BITS: categorical labels
         assert np.array_equal(o['labels'], gold['labels'])
     else:
         assert np.array_equal(o['samples'], gold['samples'])
