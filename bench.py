@@ -96,7 +96,8 @@ def main():
     import torch
     import torch.distributed as dist
     from wavernn_amd.model import WaveRNN
-    from wavernn_amd.hparams import sp, wavernn_fatchord, wavernn_runtimeracer
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_state_dict, synth_mel
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -107,8 +108,8 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
-    base = wavernn_fatchord if args.model == 'fatchord-wavernn' else wavernn_runtimeracer
-    hp = base.copy(bits=args.bits, mode=args.mode)
+    mode = 'BITS' if args.model == 'geneing-wavernn' and args.mode == 'RAW' else args.mode
+    hp = hparams_for(args.model).copy(bits=args.bits, mode=mode)
     sd = synth_state_dict(hp, args.model, seed=0)
     model = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
                     hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
