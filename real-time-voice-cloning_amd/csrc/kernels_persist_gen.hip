@@ -1,0 +1,492 @@
+// Persistent, weight-stationary recurrence of the geneing WaveRNN (PERSIST engine, third
+// topology).
+//
+// Reference step body: vocoder/models/geneing_version.py:193-205 (rnn_dims 256, fc_dims 128):
+//   x1 = I(x0) + h1'     h1' = rnn1(I(x0), h1)
+//   y1 = relu(fc1([x1, a2]))        logits = fc3(y1)
+//
+// Execution model of kernels_persist.hip / kernels_persist_rr.hip: 8 XCD-local groups of 32
+// workgroups x 512 threads, all step weights register-resident, tagged (value, step) pairs
+// exchanged through the XCD's L2. Slot w owns GRU units [8w, 8w + 8), fc1 outputs
+// [4w, 4w + 4) and fc3 classes [cpw w, cpw (w + 1)). Threads form four quads of 128
+// (og = 0..7, kc = k-chunk 0..15); host layout (pack_persist_gen):
+//   quad 0: W_hh1 rows of unit 8 w + og (3 gates x 4 float4)   @0
+//   quad 1: fc1[:, :256] row 4 w + og, og < 4 (4 float4)        @0
+//   every quad: fc3 row of class cpw w + 8 q + og (K = 128: 2 float4) @12
+// Per step, two hops lie on the dependency chain:
+//   stage 1  q1 fc1 -> y1 (hop 1)        q0 gh1 = W_hh1 h1 + b (tagged pairs, read in stage 2)
+//   stage 2  fc3 over all quads -> per-slot Gumbel-max candidates (hop 2) / MOL logits;
+//            every thread also polls this step's gh1 pairs into LDS before the candidates are
+//            published (so no producer can overwrite them first)
+// then, redundantly in every workgroup, the sample and GRU1 of the next step (rank-1 x term).
+#include "wrnn_kernels.h"
+#include "persist_common.h"
+
+namespace wrnn {
+
+namespace {
+
+constexpr int GH = 256;        // rnn_dims
+constexpr int GK4 = GH / 4;
+constexpr int GF = kGF;        // fc_dims
+constexpr int GFK4 = GF / 4;
+constexpr int GU = GH / kPM;   // GRU units per slot (8)
+constexpr int GO = GF / kPM;   // fc1 outputs per slot (4)
+constexpr int GNR = kRNR;      // max rows per group (4)
+
+// exchange area per group (floats)
+constexpr int QX_Y = 0;                                  // fc1 hop [GNR][GF] pairs
+constexpr int QX_GH = QX_Y + GNR * GF * 2;               // gh1 [GNR][3 GH] pairs
+constexpr int QX_D = QX_GH + GNR * 3 * GH * 2;           // candidates [kPM][GNR] pairs
+constexpr int QX_D_LOG = kPM * GNR * 2;
+constexpr int QX_GROUP = QX_D + QX_D_LOG + GNR * 32 + 64;  // + MOL logits [GNR][32]
+
+// LDS carve (floats)
+constexpr int L_XA = 0;                        // [GNR][GH] x1 (fc1 input)
+constexpr int L_H1 = L_XA + GNR * GH;          // [GNR][GH] h1 (W_hh1 input)
+constexpr int L_Y = L_H1 + GNR * GH;           // [GNR][GF] y1 (fc3 input)
+constexpr int L_GH = L_Y + GNR * GF;           // [GNR][3 GH] gh1 of this step (polled)
+constexpr int L_RED = L_GH + GNR * 3 * GH;     // [32][GNR][value, class]
+constexpr int L_SX = L_RED + 32 * GNR * 2;
+constexpr int L_FAIL = L_SX + 8;
+constexpr int L_DUMMY = L_SX + 12;
+constexpr int L_RI = L_SX + 16;
+constexpr int L_CB = L_RI + 6 * GNR + 4;       // b_hh1 of the slot's units [3][8]
+constexpr int L_TOTAL = L_CB + 24;
+static_assert(L_DUMMY % 2 == 0, "float2 sink");
+
+// poll NPAIR tagged pairs per row x NR rows into LDS dst[r * NPAIR + ...]
+template <int NR, int NPAIR>
+__device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, float* dst, float* sink,
+                                          unsigned* ctl, int tid) {
+    constexpr int CPR = NPAIR / 2;  // couples per row
+    constexpr int TOT = NR * CPR;
+    constexpr int M = (TOT + kPT - 1) / kPT;
+    unsigned off[M];
+    float2* d[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int c = tid + kPT * m;
+        const bool valid = c < TOT;
+        const int cc = valid ? c : c % TOT;
+        const int r = cc / CPR, cp = cc % CPR;
+        off[m] = (unsigned)((r * NPAIR + 2 * cp) * 8);
+        d[m] = valid ? reinterpret_cast<float2*>(dst + r * NPAIR) + cp : reinterpret_cast<float2*>(sink);
+    }
+    return poll_couples<M>(xr, off, so, seq, d, ctl);
+}
+
+}  // namespace
+
+template <int NR>
+__global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    const int tid = threadIdx.x;
+    // ---- group formation (as kernels_persist.hip) -------------------------------------------
+    if (tid == 0) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        const int g = x & 7;
+        s_group = g;
+        s_slot = (int)atomicAdd(a.ctl + PC_REG + g, 1u);
+        atomicAdd(a.ctl + PC_TOTAL, 1u);
+        const unsigned t0 = p_now();
+        int ok = 1;
+        while (ld_sc1_u(a.ctl + PC_TOTAL) < (unsigned)(kPG * kPM)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (p_now() - t0 > kSpinTicks) {
+                ok = 0;
+                atomicMax(a.ctl + PC_ERR, 1u);
+                break;
+            }
+        }
+        if (ok)
+            for (int i = 0; i < kPG; ++i)
+                if (ld_sc1_u(a.ctl + PC_REG + i) != (unsigned)kPM) {
+                    ok = 0;
+                    atomicMax(a.ctl + PC_ERR, 3u);
+                }
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    const int g0 = a.rb + g;
+    const int q = tid >> 7;
+    const int og = (tid >> 4) & 7, kc = tid & 15;
+    const int u = GU * w + og;                  // GRU unit of quad 0's weight rows
+    const int o = GO * w + og;                  // fc1 output of quad 1 (og < GO)
+    const int cl = 8 * q + og;                  // fc3 class within the slot
+    const int cls = a.cpw * w + cl;
+    const bool has_cls = cl < a.cpw && cls < a.n_classes;
+    const int j = tid & (GH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
+    constexpr int NRH = (NR + 1) / 2;
+    unsigned* fl = a.flags + (size_t)g * 4 * 64;
+    const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * QX_GROUP);
+
+    float4 wr[kGNW];
+    {
+        const float4* src = a.wreg + ((size_t)w * kPT + tid) * kGNW;
+#pragma unroll
+        for (int i = 0; i < kGNW; ++i) wr[i] = src[i];
+    }
+    const size_t SW = 2 * GH;
+    float h1[NRH];
+#pragma unroll
+    for (int i = 0; i < NRH; ++i) {
+        const int r = 2 * i + hs;
+        h1[i] = 0.f;
+        if (r < NR) {
+            const float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+            h1[i] = st[GH + j];
+            lds[L_XA + r * GH + j] = st[j];
+            lds[L_H1 + r * GH + j] = h1[i];
+        }
+    }
+    if (tid < 24) lds[L_CB + tid] = a.b_hh1[(tid >> 3) * GH + GU * w + (tid & 7)];
+    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid == 0) lds[L_FAIL] = 0.f;
+    const bool own = kc < NR;
+    const int lr = own ? kc : 0;
+    const int lrow = g0 + kPG * lr;
+    const float vj0 = a.v[j], vj1 = a.v[GH + j], vj2 = a.v[2 * GH + j], w0j = a.w0[j];
+    const float bcls = has_cls ? a.b_f3[cls] : 0.f;
+    const rsrc_t fcr = mk_rsrc(a.fcond);
+    const unsigned o_tid = (unsigned)j * 4u;
+    __syncthreads();
+
+    const float4* XA = reinterpret_cast<const float4*>(lds + L_XA);
+    const float4* H1 = reinterpret_cast<const float4*>(lds + L_H1);
+    const float4* Y = reinterpret_cast<const float4*>(lds + L_Y);
+    float* sink = lds + L_DUMMY;
+    const int wave = tid >> 6;
+
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
+    for (int t = a.t0; t < a.t1; ++t) {
+        const unsigned seq = (unsigned)t + 1u;
+        const bool nxt = t + 1 < a.S;
+        // ---- per-step loads: fc1 conditioning, noise, P1 / cI of step t+1 -------------------
+        float pc = 0.f, pgum = 0.f;
+        if (own) {
+            const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
+            if (q == 1 && og < GO)
+                pc = bld(fcr, (unsigned)(p_frame(lri, t, a.hop) * a.cond_width + a.oF1 + o) * 4u, 0);
+            if (has_cls && a.mode == 0)
+                pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
+                           (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+        }
+        float pP[NRH][3], pC[NRH];
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) pP[i][0] = pP[i][1] = pP[i][2] = pC[i] = 0.f;
+        if (nxt) {
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(t + 1) * a.B + g0) * 3 * GH);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(t + 1) * a.B + g0) * GH);
+#pragma unroll
+            for (int i = 0; i < NRH; ++i) {
+                const int r = 2 * i + hs;
+                if (r < NR) {
+#pragma unroll
+                    for (int jg = 0; jg < 3; ++jg)
+                        pP[i][jg] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * GH + jg * GH) * 4u);
+                    pC[i] = bld(cr, o_tid, (unsigned)(r * kPG * GH) * 4u);
+                }
+            }
+        }
+        // ================= stage 1: q1 fc1 (critical) | q0 gh1 = W_hh1 h1 + b ===============
+        if (q == 1) {
+            __builtin_amdgcn_s_setprio(2);
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                v2f acc = {0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dot4(acc, wr[i], XA[r * GK4 + 16 * i + kc]);
+                const float tt = row16_sum(hsum(acc));
+                if (kc == r) s = tt;
+            }
+            if (own && og < GO) {
+                const float y = p_add(s, pc);
+                bst_tag(y > 0.f ? y : 0.f, seq, xr, (unsigned)(lr * GF + o) * 8u, QX_Y * 4);
+            }
+            __builtin_amdgcn_s_setprio(0);
+        } else if (q == 0) {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 x4 = H1[r * GK4 + 16 * i + kc];
+#pragma unroll
+                    for (int jg = 0; jg < 3; ++jg) dot4(acc[jg], wr[4 * jg + i], x4);
+                }
+                const float t0 = row16_sum(hsum(acc[0]));
+                const float t1 = row16_sum(hsum(acc[1]));
+                const float t2 = row16_sum(hsum(acc[2]));
+                if (kc == r) {
+                    s0 = t0;
+                    s1 = t1;
+                    s2 = t2;
+                }
+            }
+            if (own) {
+                const float* cb = lds + L_CB;
+                const unsigned ob = (unsigned)(lr * 3 * GH + u) * 8u;
+                bst_tag(p_add(s0, cb[og]), seq, xr, ob, QX_GH * 4);
+                bst_tag(p_add(s1, cb[8 + og]), seq, xr, ob + GH * 8, QX_GH * 4);
+                bst_tag(p_add(s2, cb[16 + og]), seq, xr, ob + 2 * GH * 8, QX_GH * 4);
+            }
+        }
+        if (!poll_rows<NR, GF>(xr, QX_Y * 4, seq, lds + L_Y, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        // ================= stage 2: fc3 -> candidates; gh1 of this step into LDS ===========
+        {
+            float s0 = 0.f;
+            if (8 * q < a.cpw) {  // wave-uniform skip of quads without classes
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    v2f acc = {0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) dot4(acc, wr[12 + i], Y[r * GFK4 + 16 * i + kc]);
+                    const float tt = row16_sum(hsum(acc));
+                    if (kc == r) s0 = tt;
+                }
+            }
+            float* red = lds + L_RED;
+            if (own) {
+                float val = -INFINITY;
+                if (has_cls) {
+                    const float l = p_add(s0, bcls);
+                    if (a.mode == 0)
+                        val = p_add(l, pgum);
+                    else
+                        bst(l, xr, (unsigned)(kc * 32 + cls) * 4u, (QX_D + QX_D_LOG) * 4);
+                }
+                red[(cl * GNR + kc) * 2] = val;
+                red[(cl * GNR + kc) * 2 + 1] = __int_as_float(cls);
+            }
+            // this step's gh1 pairs, read before this workgroup's candidate can be seen (a
+            // producer overwrites them only after every candidate of this step is out)
+            if (!poll_rows<NR, 3 * GH>(xr, QX_GH * 4, seq, lds + L_GH, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+            __syncthreads();
+            if (lds[L_FAIL] != 0.f) return;
+            if (wave == 0) {
+                if (a.mode == 0) {
+                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    if (a.cpw <= 16) {
+                        const int r = tid >> 4, oo = tid & 15;
+                        float bv = -INFINITY;
+                        int bi = 0x7fffffff;
+                        if (r < NR && oo < a.cpw) {
+                            bv = red[(oo * GNR + r) * 2];
+                            bi = __float_as_int(red[(oo * GNR + r) * 2 + 1]);
+                        }
+                        row16_argmax(bv, bi);
+                        if (r < NR && oo == 0)
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                (unsigned)((w * GNR + r) * 2) * 4u, QX_D * 4, 0);
+                    } else {
+#pragma unroll
+                        for (int rb = 0; rb < NR; rb += 2) {
+                            const int r = rb + (tid >> 5), oo = tid & 31;
+                            float bv = -INFINITY;
+                            int bi = 0x7fffffff;
+                            if (r < NR && oo < a.cpw) {
+                                bv = red[(oo * GNR + r) * 2];
+                                bi = __float_as_int(red[(oo * GNR + r) * 2 + 1]);
+                            }
+                            half_argmax(bv, bi);
+                            if (r < NR && oo == 31)
+                                __builtin_amdgcn_raw_buffer_store_b64(
+                                    (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                    (unsigned)((w * GNR + r) * 2) * 4u, QX_D * 4, 0);
+                        }
+                    }
+                } else {  // MOL: logits rows + flag
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (tid == 0)
+                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
+        // ================= sample of step t (redundant in every workgroup) ==================
+        if (a.mode == 0) {
+            if (tid < 32 * NR) {
+                const int r = tid >> 5, oo = tid & 31;
+                const unsigned off = (unsigned)((oo * GNR + r) * 2) * 4u;
+                const unsigned want = seq & kTagSeqMask;
+                u2v c;
+                const unsigned ts = p_now();
+                unsigned n = 0;
+                while (true) {
+                    c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, QX_D * 4, kCpNT);
+                    if (__all((c.y >> 11) == want)) break;
+                    if ((++n & 255) == 0) {
+                        if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - ts > kSpinTicks) {
+                            if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                            lds[L_FAIL] = 1.f;
+                            break;
+                        }
+                    }
+                }
+                float bv = __uint_as_float(c.x);
+                int bi = (int)(c.y & 0x7ffu);
+                half_argmax(bv, bi);
+                if (oo == 31) {
+                    float xv;
+                    {
+#pragma clang fp contract(off)
+                        xv = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
+                    }
+                    lds[L_SX + r] = xv;
+                    if (w == 0) {
+                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
+                                                              ro * 2u, (unsigned)t * 2u, 0);
+                        bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                    }
+                }
+            }
+        } else if (tid < NR) {
+            // MOL: vocoder/distribution.py:104-140 with the precomputed draws of k_mol_noise
+            const int r = tid, row = g0 + kPG * r;
+            const unsigned lo = (unsigned)(r * 32) * 4u;
+            const unsigned so = (QX_D + QX_D_LOG) * 4;
+            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
+            float gm[11];
+#pragma unroll
+            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
+            float xv;
+            {
+#pragma clang fp contract(off)
+                float bv = -INFINITY;
+                int bi = 0;
+#pragma unroll
+                for (int k = 0; k < 10; ++k) {
+                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
+                    if (v2 > bv) {
+                        bv = v2;
+                        bi = k;
+                    }
+                }
+                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
+                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
+                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                ls = ls < lsmin ? lsmin : ls;
+                xv = mean + expf(ls) * gm[10];
+                xv = xv < -1.f ? -1.f : xv;
+                xv = xv > 1.f ? 1.f : xv;
+            }
+            lds[L_SX + r] = xv;
+            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+        }
+        __syncthreads();
+        if (lds[L_FAIL] != 0.f) return;
+        if (!nxt) continue;
+        // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) {
+            const int r = 2 * i + hs;
+            if (r < NR) {
+                const float x = lds[L_SX + r];
+                const float* gh = lds + L_GH + r * 3 * GH + j;
+                const float hn = p_gru(fmaf(vj0, x, pP[i][0]), fmaf(vj1, x, pP[i][1]),
+                                       fmaf(vj2, x, pP[i][2]), gh[0], gh[GH], gh[2 * GH], h1[i]);
+                h1[i] = hn;
+                lds[L_XA + r * GH + j] = p_add(fmaf(w0j, x, pC[i]), hn);
+                lds[L_H1 + r * GH + j] = hn;
+            }
+        }
+        __syncthreads();
+    }
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+    if (a.t1 < a.S && w == 0) {
+#pragma unroll
+        for (int i = 0; i < NRH; ++i) {
+            const int r = 2 * i + hs;
+            if (r < NR) {
+                float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+                st[j] = lds[L_XA + r * GH + j];
+                st[GH + j] = lds[L_H1 + r * GH + j];
+            }
+        }
+    }
+}
+
+// Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0).
+__global__ __launch_bounds__(kRH) void k_persist_gen_init(PersistGenArgs a) {
+    const int row = blockIdx.x, j = threadIdx.x, H = GH;
+    const float* P1 = a.P1 + (size_t)row * 3 * H;
+    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
+                           a.b_hh1[2 * H + j], 0.f);
+    float* st = a.st + (size_t)row * 2 * H;
+    st[j] = p_add(a.cI[(size_t)row * H + j], hn);
+    st[H + j] = hn;
+}
+
+hipError_t launch_persist_gen_init(const PersistGenArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_persist_gen_init, dim3(a.B), dim3(GH), 0, s, a);
+    return hipGetLastError();
+}
+
+// at least 96 KB so that no CU can take two workgroups of this (register-light) kernel:
+// every group must span 32 CUs
+size_t persist_gen_lds_bytes() {
+    const size_t need = (size_t)L_TOTAL * sizeof(float);
+    return need > 96 * 1024 ? need : 96 * 1024;
+}
+size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
+
+template <int NR>
+hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
+    static bool attr = false;
+    const size_t lds = persist_gen_lds_bytes();
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_persist_gen<NR>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NR>
+int persist_gen_spill_t() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+int persist_gen_variant_ok(int nr, int cpw) {
+    if (cpw < 1 || cpw > 32) return 0;
+    int sp = -1;
+    switch (nr) {
+        case 1: sp = persist_gen_spill_t<1>(); break;
+        case 2: sp = persist_gen_spill_t<2>(); break;
+        case 3: sp = persist_gen_spill_t<3>(); break;
+        case 4: sp = persist_gen_spill_t<4>(); break;
+        default: break;
+    }
+    return sp == 0 ? 1 : 0;
+}
+
+hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s) {
+    if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > 32 ||
+        a.cpw * kPM < a.n_classes || (a.mode != 0 && a.n_classes > 32))
+        return hipErrorInvalidValue;
+    switch (a.nr) {
+        case 1: return launch_persist_gen_t<1>(a, s);
+        case 2: return launch_persist_gen_t<2>(a, s);
+        case 3: return launch_persist_gen_t<3>(a, s);
+        case 4: return launch_persist_gen_t<4>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace wrnn

@@ -172,6 +172,7 @@ struct wrnn_handle {
     struct PersistW {
         bool ok = false;  // weights packed (fatchord 512 / runtimeracer 256 dims, n <= 1024)
         bool rr = false;  // runtimeracer topology (kernels_persist_rr.hip)
+        bool gen = false; // geneing topology (kernels_persist_gen.hip)
         int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;  // rr: oG2 = oG3, oF2 = oF3
         const float *wreg = nullptr, *wlds = nullptr;
         const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
@@ -388,6 +389,8 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
     auto& P = h->pw;
     P.ok = false;
+    P.rr = false;
+    P.gen = false;
     if (h->cfg.model_type != WRNN_MODEL_FATCHORD || H != kPH || F != kPH || n > kPM * kPCls)
         return WRNN_OK;
     const auto& Wih2 = T["rnn2.weight_ih_l0"];  // (3H, H + A)
@@ -468,6 +471,7 @@ int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
     auto& P = h->pw;
     P.ok = false;
     P.rr = true;
+    P.gen = false;
     if (h->cfg.model_type != WRNN_MODEL_RUNTIMERACER || H != kRH || F != kRH || n > kPM * 32)
         return WRNN_OK;
     P.cpw = (n + kPM - 1) / kPM;
@@ -525,6 +529,60 @@ int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
     P.oG2 = oG3;
     P.oF1 = oF1;
     P.oF2 = oF3;
+    P.ok = true;
+    return WRNN_OK;
+}
+
+// Geneing persistent-engine weight layout (kernels_persist_gen.hip). Slot w, thread tid
+// (quad q = tid / 128, og = (tid / 16) % 8, kc = tid % 16) holds float4 i:
+//   quad 0: W_hh1 gate j of unit 8 w + og, k-float4 16 i + kc @ 4 j + i (i < 4)
+//   quad 1: fc1[:, :256] row 4 w + og (og < 4), k-float4 16 i + kc @ i (i < 4)
+//   every quad: fc3 row of class cpw w + 8 q + og, k-float4 16 i + kc @ 12 + i (i < 2)
+int pack_persist_gen(wrnn_handle* h, int oF1) {
+    auto& T = h->host;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    auto& P = h->pw;
+    P.ok = false;
+    P.rr = false;
+    P.gen = true;
+    if (h->cfg.model_type != WRNN_MODEL_GENEING || H != kRH || F != kGF || n > kPM * 32) return WRNN_OK;
+    P.cpw = (n + kPM - 1) / kPM;
+    P.nw = kGNW;
+    std::vector<float> wreg((size_t)kPM * kPT * kGNW * 4, 0.f);
+    const auto& Whh = T["rnn1.weight_hh_l0"];
+    const auto& Wf1 = T["fc1.weight"];
+    const auto& Wf3 = T["fc3.weight"];
+    for (int w = 0; w < kPM; ++w)
+        for (int tid = 0; tid < kPT; ++tid) {
+            const int q = tid >> 7, og = (tid >> 4) & 7, kc = tid & 15;
+            float* d = wreg.data() + ((size_t)w * kPT + tid) * kGNW * 4;
+            if (q == 0)
+                for (int j = 0; j < 3; ++j)
+                    for (int i = 0; i < 4; ++i)
+                        std::memcpy(d + 4 * (4 * j + i), &Whh[(size_t)(j * H + 8 * w + og) * H + 4 * (16 * i + kc)],
+                                    4 * sizeof(float));
+            if (q == 1 && og < F / kPM)
+                for (int i = 0; i < 4; ++i)
+                    std::memcpy(d + 4 * i, &Wf1[(size_t)(F / kPM * w + og) * (H + A) + 4 * (16 * i + kc)],
+                                4 * sizeof(float));
+            const int cl = 8 * q + og, c = P.cpw * w + cl;
+            if (cl < P.cpw && c < n)
+                for (int i = 0; i < 2; ++i)
+                    std::memcpy(d + 4 * (12 + i), &Wf3[(size_t)c * F + 4 * (16 * i + kc)], 4 * sizeof(float));
+        }
+    int rc = WRNN_OK;
+    P.wreg = upload(h, wreg, &rc);
+    CHECK(rc);
+    P.wlds = nullptr;
+    CHECK(pack_p1(h));
+    auto dv = [&](const std::string& key) -> const float* {
+        if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
+        return h->dvec[key];
+    };
+    P.b_hh1 = dv("rnn1.bias_hh_l0");
+    P.b_fc3 = dv("fc3.bias");
+    CHECK(rc);
+    P.oF1 = oF1;
     P.ok = true;
     return WRNN_OK;
 }
@@ -734,6 +792,7 @@ int do_finalize(wrnn_handle* h) {
         s1.segs.push_back(seg_fc("fc3", n, F, SL_Y1, SL_LOG, false, dv("fc3.bias"), -1, F));
         CHECK(rc);
         h->stages = {s0, s1};
+        CHECK(pack_persist_gen(h, oF1));
     } else {
         h->pw.ok = false;
         h->pw.rr = false;
@@ -1310,7 +1369,8 @@ bool persist_device_ok(wrnn_handle* h) {
     hipDeviceProp_t p;
     bool ok = hipGetDeviceProperties(&p, d) == hipSuccess && p.multiProcessorCount == kPG * kPM &&
               std::strncmp(p.gcnArchName, "gfx950", 6) == 0 &&
-              p.sharedMemPerMultiprocessor >= std::max(persist_lds_bytes(), persist_rr_lds_bytes());
+              p.sharedMemPerMultiprocessor >=
+                  std::max({persist_lds_bytes(), persist_rr_lds_bytes(), persist_gen_lds_bytes()});
     if (d >= 0 && d < 64) cached[d] = ok ? 1 : 2;
     return ok;
 }
@@ -1367,10 +1427,10 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
     CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
-    const bool rr = W.rr;
-    const size_t xfl = rr ? persist_rr_xbuf_floats() : persist_xbuf_floats();
+    const bool rr = W.rr, gen = W.gen;
+    const size_t xfl = gen ? persist_gen_xbuf_floats() : rr ? persist_rr_xbuf_floats() : persist_xbuf_floats();
     CHECK(P.xbuf.alloc(xfl * sizeof(float)));
-    CHECK(P.st.alloc((size_t)Bp * (rr ? 11 * kRH : 6 * H) * sizeof(float)));
+    CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? 11 * kRH : 6 * H) * sizeof(float)));
     // P1 (all steps, rows) was written by run_upsample next to cI
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
     if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, (const RowInfo*)ws.rows.p, k0, k1, st));
@@ -1418,8 +1478,36 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(hipMemsetAsync(P.phases.p, 0, P.phases.bytes, st));
         a.phases = (uint32_t*)P.phases.p;
     }
+    PersistGenArgs ag{};
     PersistRRArgs ar{};
-    if (rr) {
+    if (gen) {
+        ag.ctl = a.ctl;
+        ag.flags = a.flags;
+        ag.xbuf = a.xbuf;
+        ag.S = S;
+        ag.B = Bp;
+        ag.mode = a.mode;
+        ag.n_classes = n;
+        ag.hop = a.hop;
+        ag.cpw = W.cpw;
+        ag.rows = a.rows;
+        ag.wreg = (const float4*)W.wreg;
+        ag.b_hh1 = W.b_hh1;
+        ag.b_f3 = W.b_fc3;
+        ag.v = h->v1;
+        ag.w0 = h->w0;
+        ag.fcond = a.fcond;
+        ag.cond_width = a.cond_width;
+        ag.oF1 = W.oF1;
+        ag.P1 = a.P1;
+        ag.cI = a.cI;
+        ag.gumbel = a.gumbel;
+        ag.labels = a.labels;
+        ag.samples = a.samples;
+        ag.ld = a.ld;
+        ag.st = P.st.f();
+        HIPC(launch_persist_gen_init(ag, st));
+    } else if (rr) {
         ar.ctl = a.ctl;
         ar.flags = a.flags;
         ar.xbuf = a.xbuf;
@@ -1505,7 +1593,14 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             h->pev_steps.push_back(a.t1 - a.t0);
             HIPC(hipEventRecord(e0, st));
         }
-        if (rr) {
+        if (gen) {
+            ag.t0 = a.t0;
+            ag.t1 = a.t1;
+            ag.nr = a.nr;
+            ag.rb = a.rb;
+            ag.stamps = a.stamps;
+            HIPC(launch_persist_gen(ag, st));
+        } else if (rr) {
             ar.t0 = a.t0;
             ar.t1 = a.t1;
             ar.nr = a.nr;
@@ -1604,13 +1699,17 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     int nr_max = 0;
     if (h->pw.ok)
         for (int r = kPNR; r >= 1 && !nr_max; --r)
-            if (h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw) : persist_variant_ok(r, h->pw.cpw)) nr_max = r;
+            if (h->pw.gen  ? persist_gen_variant_ok(r, h->pw.cpw)
+                : h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw)
+                           : persist_variant_ok(r, h->pw.cpw))
+                nr_max = r;
     const int nbatch = nr_max ? (B + kPG * nr_max - 1) / (kPG * nr_max) : 0;
     const int nr = nbatch ? (B + kPG * nbatch - 1) / (kPG * nbatch) : 0;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
         if (!h->pw.ok)
-            why = "model is not fatchord (rnn_dims = fc_dims = 512) or runtimeracer (256) with <= 1024 classes";
+            why = "model is not fatchord (512 / 512), runtimeracer (256 / 256) or geneing (256 / 128) "
+                  "with <= 1024 classes";
         else if (!nr_max) why = "no register-resident variant for this class count";
         else if ((double)S * kPG * nr * nbatch * (4 * h->H + h->n_classes) * 4.0 > kPersistWsBytes)
             why = "P1 / noise workspace for " + std::to_string(B) + " rows x " + std::to_string(S) +

@@ -248,6 +248,44 @@ struct PersistRRArgs {
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------
+// Persistent geneing recurrence (kernels_persist_gen.hip): rnn_dims 256, fc_dims 128; per
+// step fc1 (hop 1) and fc3 candidates (hop 2), W_hh1 h1 published as tagged pairs beside.
+// ---------------------------------------------------------------------------------------
+constexpr int kGF = 128;     // fc_dims
+constexpr int kGNW = 16;     // float4 weight registers per thread
+
+struct PersistGenArgs {
+    unsigned* ctl;
+    unsigned* flags;        // [kPG][4][64] (MOL hop flags)
+    float* xbuf;            // per-group exchange area (persist_gen_xbuf_floats())
+    int t0, t1, S;
+    int B, nr, rb;
+    int mode, n_classes, hop, cpw;
+    const RowInfo* rows;
+    const float4* wreg;     // [kPM][kPT][kGNW]
+    const float* b_hh1;     // [3H]
+    const float* b_f3;      // [n]
+    const float* v;         // [3H] W_ih1 . w0
+    const float* w0;        // [H]
+    const float* fcond;     // per-frame conditioning rows (fc1: W_fc1[:, H:] a2 + b_fc1)
+    int cond_width, oF1;
+    const float* P1;        // [S][B][3H]
+    const float* cI;        // [S][B][H]
+    const float* gumbel;    // RAW [S][B][n]; MOL [S][B][kMolNoise]
+    int16_t* labels;        // [B][ld]
+    float* samples;         // [B][ld]
+    int ld;
+    float* st;              // chunk state [B][2 H]: x1, h1
+    uint32_t* stamps;
+};
+
+hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s);
+hipError_t launch_persist_gen_init(const PersistGenArgs& a, hipStream_t s);
+int persist_gen_variant_ok(int nr, int cpw);
+size_t persist_gen_lds_bytes();
+size_t persist_gen_xbuf_floats();
 hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s);
 int persist_rr_variant_ok(int nr, int cpw);
 size_t persist_rr_lds_bytes();

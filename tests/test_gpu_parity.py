@@ -48,15 +48,14 @@ def first_divergence(a, b):
 
 
 def engine_cases(*modes):
-    # CHAIN runs every topology; PERSIST runs fatchord (kernels_persist.hip) and runtimeracer
-    # (kernels_persist_rr.hip)
+    # both engines run every topology (PERSIST: kernels_persist.hip fatchord,
+    # kernels_persist_rr.hip runtimeracer, kernels_persist_gen.hip geneing)
     out = []
     for k, v in golden_meta().items():
         if v['mode'] not in modes:
             continue
         out.append((k, 'chain'))
-        if v['model_type'] != 'geneing-wavernn':
-            out.append((k, 'persist'))
+        out.append((k, 'persist'))
     return out
 
 
@@ -118,7 +117,8 @@ def test_upsample_network_matches_oracle():
     np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize('case', ['fatchord_raw9_sharp_tiny', 'runtimeracer_raw9_tiny'])
+@pytest.mark.parametrize('case', ['fatchord_raw9_sharp_tiny', 'runtimeracer_raw9_tiny',
+                                  'geneing_bits10_tiny'])
 @pytest.mark.parametrize('n_utts', [3, 4, 6, 10])
 def test_persist_multi_row_groups_match_oracle(n_utts, case):
     """5 fold rows per utterance -> 15 / 20 / 30 / 50 rows: 2 and 3 rows per XCD group (the
@@ -150,7 +150,7 @@ def test_persist_multi_row_groups_match_oracle(n_utts, case):
             f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'
 
 
-@pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny'])
+@pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny', 'geneing_mol_tiny'])
 def test_persist_row_batches_mol_within_tolerance(case):
     """MOL float path over row batches (6 utterances x the case's fold rows)."""
     import torch
