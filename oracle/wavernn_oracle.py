@@ -259,12 +259,15 @@ class OracleWaveRNN:
         return mels, aux, wave_len
 
     def generate(self, mels, batched, target, overlap, mu_law, apply_preemphasis, seed=0,
-                 stream=0, max_steps=None, progress_callback=None, record_logits=None):
+                 stream=0, max_steps=None, progress_callback=None, record_logits=None,
+                 post=True):
         """Restates generate(); returns a dict with 'wav' and per-row outputs.
 
         ``mels``: torch (1, n_mels, T) float32, already divided by max_abs_value.
         ``max_steps``: stop the recurrence early (bounded CPU-baseline sample); 'wav' is
         then None.
+        ``post=False``: rows only, no post-processing ('wav' None) -- mels shorter than the
+        20-hop tail fade have rows but no waveform (the reference raises there, :253-255).
         ``record_logits``: optional list of step indices whose logits are returned.
         """
         mu_law = mu_law if self.mode == 'RAW' else False  # geneing BITS: no mu-law (:158)
@@ -314,7 +317,7 @@ class OracleWaveRNN:
         output = torch.stack(samples).transpose(0, 1)
         out['samples'] = output.numpy().copy()
         out['logits'] = logits_rec
-        if n_steps < seq_len:
+        if n_steps < seq_len or not post:
             out['wav'] = None
             return out
         t0 = time.time()
