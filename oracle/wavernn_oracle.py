@@ -9,6 +9,8 @@ What it restates (same torch ops, same order, same fp32/f64 dtypes as the refere
 
 * ``WaveRNN.generate``          vocoder/models/fatchord_version.py:155-259
                                 vocoder/models/runtimeracer_version.py:199-314
+                                vocoder/models/geneing_version.py:157-253 (I, rnn1, fc1, fc3;
+                                2-way aux split; BITS = categorical over 2**bits, no mu-law)
 * ``UpsampleNetwork.forward``   fatchord_version.py:78-85 (+ MelResNet :38-44, ResBlock :17-24,
                                 Stretch2d :53-57); runtimeracer_version.py:88-95
 * ``pad_tensor``                fatchord_version.py:275-288
