@@ -12,16 +12,16 @@
 // HBM per step except the precomputed per-step inputs (P1, cI, per-frame aux terms, Gumbel
 // noise), all issued at the top of the step so their latency hides behind the exchanges.
 //
-// Per step, four in-group exchanges (plain stores -> s_waitcnt vmcnt(0) -> workgroup barrier ->
-// one plain flag store per workgroup; consumers poll the 32 flags and read the payload with
-// non-temporal loads, which are served by the XCD's shared L2; measured stale-free and ~1.3 us
-// per hop on MI355X, tools/microbench_xcd.hip):
-//   A: GRU2 (W_ih2 x1 + cond, gh2 of the previous step) -> x2, h2 ; W_hh1 h1 + b -> gh1
-//   B: fc1 (relu) on x2                   ; W_hh2 h2 + b -> gh2 for the next step (kept local)
+// Per step, four in-group exchanges of tagged pairs (value, step + 1) stored to the group's
+// exchange area and polled with non-temporal loads served by the XCD's shared L2:
+//   A: GRU2 (W_ih2 x1 + cond, gh2 of the previous step) -> x2, h2
+//   B: fc1 (relu) on x2
 //   C: fc2 (relu) on y1
 //   D: fc3 on y2 -> per-slot Gumbel-max candidates (RAW) or logits (MOL)
-// and, redundantly in every workgroup: the sample of step t and GRU1 of step t+1 for all 512
-// units (so x1/h1 never need an exchange).
+// Each of these runs alone on the CU; the off-path products run in the exchange waits that
+// follow (behind a workgroup barrier): W_hh1 h1 + b -> gh1 (published) in hop A, W_hh2 h2 + b
+// -> gh2 of the next step (kept local) in hops B and C. Redundantly in every workgroup: the
+// sample of step t and GRU1 of step t+1 for all 512 units (so x1/h1 never need an exchange).
 // Sampling: argmax_k (l_k + g_k), g_k = -log q_k with q the RNG contract's Exp(1) variate --
 // the same decision as the reference's argmax((softmax(l)/sum)/q) in exact arithmetic.
 // Every spin is bounded; on a timeout the kernel sets an error code and every group exits.
@@ -46,17 +46,22 @@ constexpr int XB_GROUP = XB_D + XB_D_SZ + 64;
 // LDS carve (floats). The per-step operands come first so every ds_read offset of the inner
 // loops fits the 16-bit immediate (no per-(q, row) address registers).
 constexpr int L_X0 = 0;                             // [kPNR][512]
-constexpr int L_X1 = L_X0 + kPNR * kPH;             // [kPNR][512]
-constexpr int L_RED = L_X1 + kPNR * kPH;            // [32 og][kPNR][2]
+constexpr int L_X1 = L_X0 + kPNR * kPH;             // [kPNR][512] h1
+constexpr int L_XH2 = L_X1 + kPNR * kPH;            // [kPNR][512] h2 (staged at hop A)
+constexpr int L_RED = L_XH2 + kPNR * kPH;           // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
 constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
-constexpr int L_W = L_BIAS + 100;                   // slot weights (kPLdsW4 float4)
+constexpr int L_W0 = L_BIAS + 96;                    // w0 = W_ih1[:, 0] [512] (GRU1 input term)
+constexpr int L_BCLS = L_W0 + kPH;                  // b_fc3 of the slot's classes [32]
+constexpr int L_SCR = L_BCLS + kPCls;               // landing line of the L2 warm-up loads [64]
+constexpr int L_W = (L_SCR + 64 + 3) & ~3;          // slot weights (kPLdsW4 float4)
 constexpr int L_FC3 = L_W + 16 * 3 * kPH;           // fc3 rows inside the weight block
 constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
+static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
 template <int NR, bool FC3R>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
@@ -106,6 +111,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
     // stamps of wave 0 at [i], of wave 4 at [12 + i]; shader-clock cycles of the traced step
     // (wave 0) at [24] / [25] give the core clock against the 100 MHz stamps
+#define XSTAMP(i)                                                        \
+    if (trace && t == a.phase_t && tid == 0) ph[(i)] = p_now();
 #define PSTAMP(i)                                                        \
     if (trace && t == a.phase_t && (tid & 255) == 0) {                   \
         ph[(tid >> 8) * 12 + (i)] = p_now();                             \
@@ -145,9 +152,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_GH2 + (og * 3 + j) * kPNR + kc] = a.st_gh2[(size_t)lrow * 3 * H + j * H + u];
     }
     // per-thread constants
-    const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid], w0j = a.w0[tid];
+    // (w0 and b_fc3 wait in LDS: read once per step each, they need no register)
+    const float vj0 = a.v[tid], vj1 = a.v[H + tid], vj2 = a.v[2 * H + tid];
+    lds[L_W0 + tid] = a.w0[tid];
     if (tid < 96) lds[L_BIAS + tid] = (tid < 48 ? a.b_hh1 : a.b_hh2)[(tid % 48 / 16) * H + 16 * w + (tid & 15)];
-    const float bcls = has_cls ? a.b_fc3[cls] : 0.f;
+    if ((tid & 15) == 0) lds[L_BCLS + og] = has_cls ? a.b_fc3[cls] : 0.f;
     if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
     // per-lane byte offsets (32-bit)
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
@@ -155,12 +164,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const unsigned o_y = (unsigned)(lr * kPH + u) * 8u;                 // bufB/C pair (row lr, unit u)
     const unsigned o_gum = (unsigned)(lrow * a.n_classes + cls) * 4u;   // gumbel row lrow
     const rsrc_t fcr = mk_rsrc(a.fcond);
-    const unsigned o_fc = (unsigned)((gate_a ? a.oG2 : a.oF1) + u) * 4u;
-    const unsigned o_f2 = (unsigned)(a.oF2 + u) * 4u;
     __syncthreads();
 
     const float4* X0 = reinterpret_cast<const float4*>(lds + L_X0);
     const float4* X1 = reinterpret_cast<const float4*>(lds + L_X1);
+    const float4* XH2 = reinterpret_cast<const float4*>(lds + L_XH2);
     const int wave = tid >> 6;
     const bool wv_lo = wave < 4;  // waves 0-3: og < 16 (GRU2, hh2, fc2, fc3 <= 16 classes)
     // Per-step operands, issued right after the wave's last publish of the previous step
@@ -170,12 +178,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     //   pgn    Gumbel noise of step te, class cls (copied to pgum at the end of step te-1)
     float pP[NR][3], pC[NR];
     float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f, pgn = 0.f;
+    // Loads are unconditional (step indices clamped; past the last step the values go
+    // unused): every path to the loop's back edge then consumes them, so the compiler's
+    // wait insertion sees no load pending at the top of the step.
     auto prefetch = [&](int tg, int te) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r) pP[r][0] = pP[r][1] = pP[r][2] = pC[r] = 0.f;
-        if (tg + 1 < a.S) {
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(tg + 1) * a.B + g0) * 3 * H);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(tg + 1) * a.B + g0) * H);
+        {
+            const int tn = tg + 1 < a.S ? tg + 1 : a.S - 1;
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * H);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * H);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
 #pragma unroll
@@ -184,7 +194,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pC[r] = bld(cr, o_tid, (unsigned)(r * kPG * H) * 4u);
             }
         }
-        if (kc < NR && te < a.S) {
+        te = te < a.S ? te : a.S - 1;
+        if (kc < NR) {
+            int uu = u;  // (offsets recomputed per step: hoisted ones cost registers)
+            asm volatile("" : "+v"(uu));
+            const unsigned o_fc = (unsigned)((gate_a ? a.oG2 : a.oF1) + uu) * 4u;
+            const unsigned o_f2 = (unsigned)(a.oF2 + uu) * 4u;
             const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
             const unsigned fo = (unsigned)(p_frame(lri, te, a.hop) * a.cond_width) * 4u;
             pc0 = bld(fcr, o_fc + fo, 0);
@@ -202,39 +217,41 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // publish so no exchange waits on them.
     const int lines_g = a.mode == 0 ? a.n_classes / 32 : 1;
     const int lines_r = 48 + 16 + lines_g;
-    float tv = 0.f;  // result of this thread's warm-up load; consumed at the end of the step
+    // (LDS-DMA loads into a scratch line: the warm-up holds no register and nothing waits on it)
     auto touch = [&](int tt) {
         const int i = tid - 256;
         const int li = w + kPM * i;
         if (tt >= a.S || i < 0 || li >= NR * lines_r) return;
         const int r = li / lines_r, l = li % lines_r, row = g0 + kPG * r;
+        float* scr = lds + L_SCR;
         if (l < 48)
-            tv = bld(mk_rsrc(a.P1 + ((size_t)tt * a.B + row) * 3 * H), (unsigned)l * 128u, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.P1 + (size_t)tt * a.B * 3 * H), scr, 4,
+                                                     (unsigned)(row * 3 * H + l * 32) * 4u, 0, 0, 0);
         else if (l < 64)
-            tv = bld(mk_rsrc(a.cI + ((size_t)tt * a.B + row) * H), (unsigned)(l - 48) * 128u, 0);
-        else
-            tv = bld(mk_rsrc(a.gumbel + ((size_t)tt * a.B + row) * (a.mode == 0 ? a.n_classes : kMolNoise)),
-                     (unsigned)(l - 64) * 128u, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.cI + (size_t)tt * a.B * H), scr, 4,
+                                                     (unsigned)(row * H + (l - 48) * 32) * 4u, 0, 0, 0);
+        else {
+            const int gw = a.mode == 0 ? a.n_classes : kMolNoise;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.gumbel + (size_t)tt * a.B * gw), scr, 4,
+                                                     (unsigned)(row * gw + (l - 64) * 32) * 4u, 0, 0, 0);
+        }
     };
     if (tid == 0) lds[L_FAIL] = 0.f;
     prefetch(a.t0, a.t0);
     pgum = pgn;
     touch(a.t0 + 1);
     __syncthreads();
-    // gh2 rows computed in stage B by waves 0-3 (r < NRB) and in stage C by waves 4-7
-    constexpr int NRB = NR - NR / 3;
     const int tl = tid & 255;  // index inside the half that stages
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
         const unsigned seq = (unsigned)t + 1u;
         const unsigned sA = (unsigned)(XB_A + (t & 1) * XB_A_SZ) * 4u;  // bufA of this step
-        const bool nxt = t + 1 < a.S;
         PSTAMP(0);
-        // ================= stage A: GRU2 (waves 0-3, critical) | W_hh1 h1 (waves 4-7) =======
-        if (wv_lo) __builtin_amdgcn_s_setprio(2);
-        {
-            const float4* Xs = gate_a ? X0 : X1;
-            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        // Each matrix-vector product on the critical path runs alone on the CU: the off-path
+        // ones (W_hh1 h1, W_hh2 h2) are placed behind a workgroup barrier into the exchange
+        // waits that follow it, so they never compete for VALU issue or LDS bandwidth.
+        // 3-gate product of this thread's register rows (wr[0..23]) with the rows of Xs
+        auto mv3 = [&](const float4* Xs, float& s0, float& s1, float& s2) {
 #pragma unroll
             for (int r = 0; r < NR; ++r) {  // weights are register-resident: row-outer
                 v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
@@ -258,6 +275,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     s2 = t2;
                 }
             }
+        };
+        // ================= stage A: GRU2 (waves 0-3, critical) | W_hh1 h1 + b -> gh1 (4-7) ====
+        {
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3(gate_a ? X0 : X1, s0, s1, s2);
+            XSTAMP(29);
             if (kc < NR) {
                 if (gate_a) {
                     const float* gh2 = lds + L_GH2 + og * 3 * kPNR + kc;
@@ -273,28 +296,25 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     bst_tag(p_add(s2, b[32]), seq, xr, o_u, sA + 4 * kPH * 8);
                 }
             }
-            if (!gate_a) {  // gh1 must be in L2 before this wave's y1 (stage B) can be seen
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
         }
-        __builtin_amdgcn_s_setprio(0);
+        XSTAMP(30);
         PSTAMP(1);
-        // ================= stage B: fc1 (waves 4-7, critical) | W_hh2 h2 rows < NRB (0-3) ===
-        if (wv_lo) {  // stage x2 -> X0, h2 -> X1 (polling the tagged pairs, one pass)
+        // ===== hop A: stage x2 -> X0, h2 -> XH2 (waves 0-3) ======================================
+        if (wv_lo) {  // polling the tagged pairs, one pass
             unsigned off[2 * NR];
             float2* dst[2 * NR];
 #pragma unroll
             for (int m = 0; m < 2 * NR; ++m) {  // couple tl of (row m / 2, array m % 2)
                 off[m] = (unsigned)(((m >> 1) * 5 + (m & 1)) * kPH + 2 * tl) * 8u;
-                dst[m] = reinterpret_cast<float2*>(lds + ((m & 1) ? L_X1 : L_X0) + (m >> 1) * kPH) + tl;
+                dst[m] = reinterpret_cast<float2*>(lds + ((m & 1) ? L_XH2 : L_X0) + (m >> 1) * kPH) + tl;
             }
             if (!poll_couples<2 * NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(2);
-        if (!gate_a) {
-            __builtin_amdgcn_s_setprio(2);
+        // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
+        auto mv1 = [&](float bias) {
             float s0 = 0.f;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
@@ -311,19 +331,25 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 const float t0 = row16_sum(hsum(acc));
                 if (kc == r) s0 = t0;
             }
-            if (kc < NR) {
-                const float y = p_add(s0, pc0);
-                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_y, XB_B * 4);
-            }
-            __builtin_amdgcn_s_setprio(0);
+            const float y = p_add(s0, bias);
+            return y > 0.f ? y : 0.f;
+        };
+        // ================= stage B: fc1 (waves 4-7, critical) ================================
+        if (!gate_a) {
+            const float y = mv1(pc0);
+            // gh1 (hop A) must be in L2 before this wave's y1 can be seen
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
             touch(t + 2);
         }
-        // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path: rows r < NRB by
-        // waves 0-3 here, the rest by waves 4-7 in stage C (LDS weights, h2 staged in X1)
-        auto hh2_rows = [&](int r0, int r1, int ul) {
+        // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path, spread over the
+        // exchange waits: rows r % 3 == 0 by waves 0-3 in hop B, r % 3 == 1 by waves 4-7 in hop
+        // C, r % 3 == 2 by waves 4-7 in hop D (LDS weights, h2 staged in XH2)
+        auto hh2_rows = [&](auto win_c, int ul) {
+            constexpr int WIN = decltype(win_c)::value;
             const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)ul * 3 * kPK4;
-            // weights read from LDS once per step, all of the rows accumulated per weight load
-            // (each accumulator sums in the same k order as a per-row loop would)
+            // weights read from LDS once per window, the window's rows accumulated per weight
+            // load (each accumulator sums in the same k order as a per-row loop would)
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             v2f acc[NR][3];
 #pragma unroll
@@ -338,15 +364,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    if (r < r0 || r >= r1) continue;
-                    const float4 x4 = X1[r * kPK4 + 16 * q + kc];
+                    if (r % 3 != WIN) continue;
+                    const float4 x4 = XH2[r * kPK4 + 16 * q + kc];
 #pragma unroll
                     for (int j = 0; j < 3; ++j) dot4(acc[r][j], w4[j], x4);
                 }
             }
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                if (r < r0 || r >= r1) continue;
+                if (r % 3 != WIN) continue;
                 const float t0 = row16_sum(hsum(acc[r][0]));
                 const float t1 = row16_sum(hsum(acc[r][1]));
                 const float t2 = row16_sum(hsum(acc[r][2]));
@@ -356,7 +382,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     s2 = t2;
                 }
             }
-            if (kc >= r0 && kc < r1) {
+            if (kc < NR && kc % 3 == WIN) {
                 float* gh2 = lds + L_GH2 + ul * 3 * kPNR + kc;
                 const float* b = lds + L_BIAS + 48 + ul;  // b_hh2 of unit 16 w + ul
                 gh2[0] = p_add(s0, b[0]);
@@ -364,10 +390,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 gh2[2 * kPNR] = p_add(s2, b[32]);
             }
         };
-        if (gate_a) hh2_rows(0, NRB, og);
         PSTAMP(3);
-        // ================= stage C: fc2 (waves 0-3, critical) | W_hh2 h2 rows >= NRB (4-7) ===
-        if (!wv_lo) {  // stage y1 -> X0
+        __syncthreads();  // fc1 has read X0: y1 may be staged over it
+        // ===== hop B: stage y1 -> X0 (waves 4-7) | W_hh2 h2 rows r % 3 == 0 (waves 0-3) =======
+        if (!wv_lo) {
             unsigned off[NR];
             float2* dst[NR];
 #pragma unroll
@@ -376,39 +402,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
             }
             if (!poll_couples<NR>(xr, off, XB_B * 4, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+        } else {
+            hh2_rows(std::integral_constant<int, 0>(), og);
+            XSTAMP(31);
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(4);
+        // ================= stage C: fc2 (waves 0-3, critical) ================================
         if (gate_a) {
-            __builtin_amdgcn_s_setprio(2);
-            float s0 = 0.f;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                v2f acc = {0.f, 0.f};
-#pragma unroll
-                for (int qb = 0; qb < 8; qb += 4) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    float4 xq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dot4(acc, wr[24 + qb + q], xq[q]);
-                }
-                const float t0 = row16_sum(hsum(acc));
-                if (kc == r) s0 = t0;
-            }
-            if (kc < NR) {
-                const float y = p_add(s0, pf2);
-                bst_tag(y > 0.f ? y : 0.f, seq, xr, o_y, XB_C * 4);
-            }
-            __builtin_amdgcn_s_setprio(0);
-        } else {
-            hh2_rows(NRB, NR, og - 16);
+            const float y = mv1(pf2);
+            if (kc < NR) bst_tag(y, seq, xr, o_y, XB_C * 4);
         }
         PSTAMP(5);
-        // ================= stage D: fc3 -> per-slot candidates ==============================
-        if (wv_lo) {  // stage y2 -> X0
+        __syncthreads();  // fc2 has read X0: y2 may be staged over it
+        // ===== hop C: stage y2 -> X0 (waves 0-3) | W_hh2 h2 rows r % 3 == 1 (waves 4-7) =======
+        if (wv_lo) {
             unsigned off[NR];
             float2* dst[NR];
 #pragma unroll
@@ -417,6 +426,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
             }
             if (!poll_couples<NR>(xr, off, XB_C * 4, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+        } else {
+            if (NR > 1) hh2_rows(std::integral_constant<int, 1>(), og - 16);
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -434,9 +445,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             prefetch(t, t + 1);  // pgn, not pgum: the fc3 epilogue still reads pgum
         };
 
+        // At <= 16 classes per slot waves 4-7 hold no fc3 class: they issue their GRU1 loads
+        // while waves 0-3 compute fc3 (LDS only) and later poll the candidates; waves 0-3
+        // issue theirs after the candidate publish, off the critical path (a wave polls only
+        // with no bulk loads in flight: its first poll would wait for all of them).
+        constexpr bool EARLY = !FC3R;
+        const int st = EARLY ? tid - 256 : tid;  // sampling lanes: st in [0, 32 NR)
         {
             float s0 = 0.f;
-            if (has_cls) {
+            auto fc3 = [&]() {
+                if (!has_cls) return;
                 const float4* Wf = reinterpret_cast<const float4*>(lds + L_FC3) + (size_t)og * kPK4;
                 v2f acc[NR];
 #pragma unroll
@@ -461,13 +479,23 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     const float t0 = row16_sum(hsum(acc[r]));
                     if (kc == r) s0 = t0;
                 }
+            };
+            // (separate paths, so the GRU1 operands of waves 4-7 hold no register during fc3)
+            if (EARLY) {
+                if (wv_lo) {
+                    fc3();
+                    XSTAMP(26);
+                } else {
+                    gru1_loads();
+                }
+            } else {
+                fc3();
             }
-            if (!FC3R) gru1_loads();  // (10-bit: after the argmax, register budget)
             float* red = lds + L_RED;  // [og][r][value, class]
             if (kc < NR) {
                 float val = -INFINITY;
                 if (has_cls) {
-                    const float l = p_add(s0, bcls);
+                    const float l = p_add(s0, lds[L_BCLS + og]);
                     if (a.mode == 0)
                         val = p_add(l, pgum);
                     else  // MOL: logits row (og == 0 -> wave 0)
@@ -476,14 +504,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 red[(og * kPNR + kc) * 2] = val;
                 red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
             }
+            XSTAMP(28);
             __syncthreads();
             PSTAMP(11);
+            if (wv_lo) {
             if (wave == 0) {
                 if (a.mode == 0) {
                     // slot candidate per row, tagged with the step (no flag, no wait)
                     const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
+                    asm volatile("" : "+v"(tt));
                     if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
-                        const int r = tid >> 4, o = tid & 15;
+                        const int r = tt >> 4, o = tt & 15;
                         float bv = -INFINITY;
                         int bi = 0x7fffffff;
                         if (r < NR && o < a.cpw) {
@@ -491,14 +523,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                             bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                         }
                         row16_argmax(bv, bi);
+                        const int rr = r;
                         if (r < NR && o == 0)
                             __builtin_amdgcn_raw_buffer_store_b64(
                                 (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                (unsigned)((w * kPNR + r) * 2) * 4u, XB_D * 4, 0);
+                                (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
                     } else {
 #pragma unroll
                         for (int rb = 0; rb < NR; rb += 2) {
-                            const int r = rb + (tid >> 5), o = tid & 31;
+                            const int r = rb + (tt >> 5), o = tt & 31;
                             float bv = -INFINITY;
                             int bi = 0x7fffffff;
                             if (r < NR && o < a.cpw) {
@@ -506,10 +539,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                                 bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                             }
                             half_argmax(bv, bi);
+                            const int rr = r;
                             if (r < NR && o == 31)
                                 __builtin_amdgcn_raw_buffer_store_b64(
                                     (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                    (unsigned)((w * kPNR + r) * 2) * 4u, XB_D * 4, 0);
+                                    (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
                         }
                     }
                 } else {  // MOL: logits rows + flag
@@ -518,15 +552,23 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                         __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
+            if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
+                gru1_loads();
+                XSTAMP(27);
+            }
+            } else if (NR > 2) {
+                // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
+                hh2_rows(std::integral_constant<int, 2>(), og - 16);
+            }
         }
         if (FC3R) gru1_loads();
         PSTAMP(7);
-        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
+        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, st)) return;
         PSTAMP(8);
         // ================= sample of step t (redundant in every workgroup) ==================
         if (a.mode == 0) {
-            if (tid < 32 * NR) {  // half-wave r: lane o polls slot o's tagged candidate of row r
-                const int r = tid >> 5, o = tid & 31;
+            if (st >= 0 && st < 32 * NR) {  // half-wave r: lane o polls slot o's candidate of row r
+                const int r = st >> 5, o = st & 31;
                 const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
                 const unsigned want = seq & kTagSeqMask;
                 u2v c;
@@ -554,17 +596,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     }
                     lds[L_SX + r] = xv;
                     if (w == 0) {
-                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        int rr = r;  // (recomputed per step: a hoisted offset costs a register)
+                        asm volatile("" : "+v"(rr));
+                        const unsigned ro = (unsigned)((g0 + kPG * rr) * a.ld);
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
                                                               ro * 2u, (unsigned)t * 2u, 0);
                         bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
                     }
                 }
             }
-        } else if (tid < NR) {
+        } else if (st >= 0 && st < NR) {
             // MOL: vocoder/distribution.py:104-140; the Philox draws were turned into
             // gm_k = log(-log(u1_k)) and lu = log(u2) - log(1 - u2) by k_mol_noise
-            const int r = tid, row = g0 + kPG * r;
+            const int r = st, row = g0 + kPG * r;
             const unsigned lo = (unsigned)(r * 64) * 4u;
             const unsigned so = (XB_D + XB_D_LOG) * 4;
             const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
@@ -598,9 +642,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(9);
-        if (!nxt) continue;
+        // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
         // ================= GRU1 of step t+1 for all 512 units (redundant) ===================
         //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
+        const float w0j = lds[L_W0 + tid];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const float x = lds[L_SX + r];
@@ -610,27 +655,31 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X0 + r * kPH + tid] = p_add(fmaf(w0j, x, pC[r]), hn);
             lds[L_X1 + r * kPH + tid] = hn;
         }
-        asm volatile("" ::"v"(tv));  // the L2 warm-up load retires here at the latest
         pgum = pgn;
         __syncthreads();
         PSTAMP(10);
     }
 #undef PSTAMP
+#undef XSTAMP
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
     // ---- save the chunk state --------------------------------------------------------------
+    // (addresses recomputed here: values kept alive across the step loop cost registers)
     if (a.t1 < a.S) {
+        int tx = tid;
+        asm volatile("" : "+v"(tx));
+        const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15), rx = g0 + kPG * (kx < NR ? kx : 0);
         if (w == 0)
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const int row = g0 + kPG * r;
-                a.st_x1[(size_t)row * H + tid] = lds[L_X0 + r * kPH + tid];
-                a.st_h1[(size_t)row * H + tid] = lds[L_X1 + r * kPH + tid];
+                a.st_x1[(size_t)row * H + tx] = lds[L_X0 + r * kPH + tx];
+                a.st_h1[(size_t)row * H + tx] = lds[L_X1 + r * kPH + tx];
             }
         if (own) {
-            a.st_h2[(size_t)lrow * H + u] = h2r;
+            a.st_h2[(size_t)rx * H + ux] = h2r;
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-                a.st_gh2[(size_t)lrow * 3 * H + j * H + u] = lds[L_GH2 + (og * 3 + j) * kPNR + kc];
+                a.st_gh2[(size_t)rx * 3 * H + j * H + ux] = lds[L_GH2 + (og * 3 + j) * kPNR + kc];
         }
     }
 }

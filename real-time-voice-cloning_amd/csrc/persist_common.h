@@ -77,9 +77,10 @@ __device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
 }
 
 __device__ __forceinline__ bool p_wait(const unsigned* f, unsigned target, unsigned* ctl, int tid) {
-    // wave 0 polls the group's 32 flags; every wave then meets at the barrier
+    // the wave of tid 0..63 polls the group's 32 flags (callers pass tid relative to the
+    // polling wave); every wave then meets at the barrier
     __shared__ int s_fail;
-    if (tid < 64) {
+    if (tid >= 0 && tid < 64) {
         const unsigned t0 = p_now();
         unsigned n = 0;
         bool ok = true;

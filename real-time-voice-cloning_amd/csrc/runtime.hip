@@ -1403,8 +1403,26 @@ void persist_phase_report(wrnn_handle* h, int t) {
             med[wv] = d[d.size() / 2];
             mxx[wv] = d.back();
         }
-        std::fprintf(stderr, "  %-7s med %6.2f max %6.2f | med %6.2f max %6.2f\n", names[i], med[0], mxx[0], med[1],
-                     mxx[1]);
+        // and each workgroup's own timeline (from its own start), median over all workgroups
+        std::vector<double> own;
+        for (int gw = 0; gw < kPG * kPM; ++gw) {
+            const uint32_t s0 = ph[(size_t)gw * kPPhases], v = ph[(size_t)gw * kPPhases + i];
+            if (s0 && v) own.push_back(((long long)v - (long long)s0) * 0.01);
+        }
+        std::sort(own.begin(), own.end());
+        std::fprintf(stderr, "  %-7s med %6.2f max %6.2f | med %6.2f max %6.2f | own wave 0 %6.2f\n", names[i],
+                     med[0], mxx[0], med[1], mxx[1], own.empty() ? 0.0 : own[own.size() / 2]);
+    }
+    // optional extra wave-0 stamps at [26, 32) (kernel experiments), own timeline
+    for (int i = 26; i < kPPhases; ++i) {
+        std::vector<double> own;
+        for (int gw = 0; gw < kPG * kPM; ++gw) {
+            const uint32_t s0 = ph[(size_t)gw * kPPhases], v = ph[(size_t)gw * kPPhases + i];
+            if (s0 && v) own.push_back(((long long)v - (long long)s0) * 0.01);
+        }
+        if (own.empty()) continue;
+        std::sort(own.begin(), own.end());
+        std::fprintf(stderr, "  x%-6d own wave 0 med %6.2f max %6.2f\n", i, own[own.size() / 2], own.back());
     }
     {
         // core clock of workgroup 0: shader cycles / 100 MHz ticks over the traced step

@@ -8,7 +8,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = 'libwavernn_mi355x.so'
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+# WRNN_LIB: another build of the same library (kernel A/B experiments, tools/)
+LIB_PATH = os.environ.get('WRNN_LIB') or os.path.join(_HERE, LIB_NAME)
 
 WRNN_OK = 0
 WRNN_ERR_INVALID = -1
