@@ -113,6 +113,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // (wave 0) at [24] / [25] give the core clock against the 100 MHz stamps
 #define XSTAMP(i)                                                        \
     if (trace && t == a.phase_t && tid == 0) ph[(i)] = p_now();
+#ifndef WRNN_PQB3  // float4 per row per LDS batch of the 3-gate / 1-gate products
+#define WRNN_PQB3 2
+#endif
+#ifndef WRNN_PQB1
+#define WRNN_PQB1 2
+#endif
 #define PSTAMP(i)                                                        \
     if (trace && t == a.phase_t && (tid & 255) == 0) {                   \
         ph[(tid >> 8) * 12 + (i)] = p_now();                             \
@@ -251,24 +257,36 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // ones (W_hh1 h1, W_hh2 h2) are placed behind a workgroup barrier into the exchange
         // waits that follow it, so they never compete for VALU issue or LDS bandwidth.
         // 3-gate product of this thread's register rows (wr[0..23]) with the rows of Xs
+        // Matrix-vector products: k-outer in batches of QB float4 per row with every row's
+        // loads of a batch in flight together (one LDS round trip per batch, not per row);
+        // each row still accumulates in k order, as a row-outer loop would.
         auto mv3 = [&](const float4* Xs, float& s0, float& s1, float& s2) {
+            constexpr int QB = WRNN_PQB3;
+            v2f acc[NR][3];
 #pragma unroll
-            for (int r = 0; r < NR; ++r) {  // weights are register-resident: row-outer
-                v2f acc[3] = {(v2f){0.f, 0.f}, (v2f){0.f, 0.f}, (v2f){0.f, 0.f}};
+            for (int r = 0; r < NR; ++r)
 #pragma unroll
-                for (int qb = 0; qb < 8; qb += 4) {  // LDS loads in batches of 4 (latency)
-                    __builtin_amdgcn_sched_barrier(0);
-                    float4 xq[4];
+                for (int j = 0; j < 3; ++j) acc[r][j] = (v2f){0.f, 0.f};
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) xq[q] = Xs[r * kPK4 + 16 * (qb + q) + kc];
+            for (int qb = 0; qb < 8; qb += QB) {
+                __builtin_amdgcn_sched_barrier(0);
+                float4 xq[NR][QB];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
+                for (int r = 0; r < NR; ++r)
 #pragma unroll
-                        for (int j = 0; j < 3; ++j) dot4(acc[j], wr[j * 8 + qb + q], xq[q]);
-                }
-                const float t0 = row16_sum(hsum(acc[0]));
-                const float t1 = row16_sum(hsum(acc[1]));
-                const float t2 = row16_sum(hsum(acc[2]));
+                    for (int q = 0; q < QB; ++q) xq[r][q] = Xs[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+#pragma unroll
+                    for (int q = 0; q < QB; ++q)
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) dot4(acc[r][j], wr[j * 8 + qb + q], xq[r][q]);
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float t0 = row16_sum(hsum(acc[r][0]));
+                const float t1 = row16_sum(hsum(acc[r][1]));
+                const float t2 = row16_sum(hsum(acc[r][2]));
                 if (kc == r) {
                     s0 = t0;
                     s1 = t1;
@@ -315,20 +333,27 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         PSTAMP(2);
         // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
         auto mv1 = [&](float bias) {
+            constexpr int QB = WRNN_PQB1;
             float s0 = 0.f;
+            v2f acc[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+#pragma unroll
+            for (int qb = 0; qb < 8; qb += QB) {
+                __builtin_amdgcn_sched_barrier(0);
+                float4 xq[NR][QB];
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+#pragma unroll
+                    for (int q = 0; q < QB; ++q) xq[r][q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+#pragma unroll
+                    for (int q = 0; q < QB; ++q) dot4(acc[r], wr[24 + qb + q], xq[r][q]);
+            }
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                v2f acc = {0.f, 0.f};
-#pragma unroll
-                for (int qb = 0; qb < 8; qb += 4) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    float4 xq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) xq[q] = X0[r * kPK4 + 16 * (qb + q) + kc];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dot4(acc, wr[24 + qb + q], xq[q]);
-                }
-                const float t0 = row16_sum(hsum(acc));
+                const float t0 = row16_sum(hsum(acc[r]));
                 if (kc == r) s0 = t0;
             }
             const float y = p_add(s0, bias);
