@@ -178,11 +178,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                            (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
         }
         float pP[NRH][3], pC[NRH];
-#pragma unroll
-        for (int i = 0; i < NRH; ++i) pP[i][0] = pP[i][1] = pP[i][2] = pC[i] = 0.f;
-        if (nxt) {
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(t + 1) * a.B + g0) * 3 * GH);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(t + 1) * a.B + g0) * GH);
+        {  // (unconditional, step clamped: every path to the back edge consumes these loads)
+            const int tn = nxt ? t + 1 : t;
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * GH);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * GH);
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
@@ -387,7 +386,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
-        if (!nxt) continue;
+        // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
         // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
 #pragma unroll
         for (int i = 0; i < NRH; ++i) {

@@ -392,11 +392,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         // P1 / cI of step t+1 for the same GRU1 (HBM latency hides behind stages 4-8)
         float pP[NRH][3], pC[NRH];
-#pragma unroll
-        for (int i = 0; i < NRH; ++i) pP[i][0] = pP[i][1] = pP[i][2] = pC[i] = 0.f;
-        if (nxt) {
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)(t + 1) * a.B + g0) * 3 * RH);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)(t + 1) * a.B + g0) * RH);
+        {  // (unconditional, step clamped: every path to the back edge consumes these loads)
+            const int tn = nxt ? t + 1 : t;
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * RH);
+            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * RH);
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
@@ -603,7 +602,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
-        if (!nxt) continue;
+        // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
         // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
 #pragma unroll
         for (int i = 0; i < NRH; ++i) {
@@ -621,33 +620,37 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     }
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
     // ---- save the chunk state ----------------------------------------------------------------
+    // (lane indices recomputed here: values kept alive across the step loop cost registers)
     if (a.t1 < a.S) {
+        int tx = tid;
+        asm volatile("" : "+v"(tx));
+        const int jx = tx & (RH - 1), hx = tx >> 8, kx = tx & 15;
+        const int ux = RU * w + ((tx >> 4) & 7), rx = g0 + kPG * (kx < NR ? kx : 0);
         if (w == 0)
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
-                const int r = 2 * i + hs;
+                const int r = 2 * i + hx;
                 if (r < NR) {
                     float* st = a.st + (size_t)(g0 + kPG * r) * SW;
-                    st[j] = lds[L_XA + r * RH + j];
-                    st[RH + j] = lds[L_H1 + r * RH + j];
+                    st[jx] = lds[L_XA + r * RH + jx];
+                    st[RH + jx] = lds[L_H1 + r * RH + jx];
                 }
             }
         if (own) {
-            float* st = a.st + (size_t)lrow * SW;
+            float* st = a.st + (size_t)rx * SW;
             if (q == 0) {
-                st[2 * RH + u] = h2r;
-                st[3 * RH + u] = h3r;
+                st[2 * RH + ux] = h2r;
+                st[3 * RH + ux] = h3r;
 #pragma unroll
                 for (int jg = 0; jg < 3; ++jg) {
-                    st[5 * RH + jg * RH + u] = lds[L_GH2 + (jg * RU + og) * kRNR + kc];
-                    st[8 * RH + jg * RH + u] = lds[L_GH3 + (jg * RU + og) * kRNR + kc];
+                    st[5 * RH + jg * RH + ux] = lds[L_GH2 + (jg * RU + og) * kRNR + kc];
+                    st[8 * RH + jg * RH + ux] = lds[L_GH3 + (jg * RU + og) * kRNR + kc];
                 }
             } else if (q == 1) {
-                st[4 * RH + u] = h4r;
+                st[4 * RH + ux] = h4r;
             }
         }
-    }
-}
+    }}
 
 // Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0); h2 = h3 = h4 = 0,
 // gh2 = b_hh2, gh3 = b_hh3.

@@ -5,9 +5,9 @@ set -u
 mkdir -p gpurun_out/ab
 export PYTHONUNBUFFERED=1
 for lib in "$@"; do
-  n=$(basename "$lib" .so)
+  n=$(basename "$lib" .so)${TAG:-}
   WRNN_LIB=$PWD/$lib WRNN_PHASE_STEP=${PHASE_STEP:-600} timeout -k 10 200 \
-    python bench.py --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/ab/$n.phase 2>&1
+    python bench.py --steps 1 --warmup 0 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/ab/$n.phase 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "$n phase rc=$rc"; tail -5 gpurun_out/ab/$n.phase; exit $rc; }
   WRNN_LIB=$PWD/$lib timeout -k 10 200 \
     python bench.py --steps ${BSTEPS:-3} --warmup 1 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/ab/$n.bench 2>&1
