@@ -596,12 +596,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 const int r = st >> 5, o = st & 31;
                 const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
                 const unsigned want = seq & kTagSeqMask;
-                u2v c;
                 const unsigned t0 = p_now();
                 unsigned n = 0;
-                while (true) {
-                    c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
+                u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
+                while (true) {  // two polls in flight (see poll_couples)
+                    const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
                     if (__all((c.y >> 11) == want)) break;
+                    c = c1;
                     if ((++n & 255) == 0) {
                         if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
                             if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);

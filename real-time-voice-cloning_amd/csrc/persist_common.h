@@ -181,11 +181,14 @@ template <int M>
 __device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M], unsigned so,
                                              unsigned want, float2* const (&dst)[M], unsigned* ctl) {
     // spin on the first couple only (a thread's couples all come from one producer slot), then
-    // take the whole set and verify every tag; keeps the polling traffic in L2 small
+    // take the whole set and verify every tag; keeps the polling traffic in L2 small. Two
+    // polls stay in flight (the next is issued before the previous is checked), so a landed
+    // value is seen about half an L2 round trip sooner than with one poll at a time.
     const unsigned t0 = p_now();
     unsigned n = 0;
+    u4v c0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off[0], so, kCpNT);
     while (true) {
-        const u4v c0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off[0], so, kCpNT);
+        const u4v c1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off[0], so, kCpNT);
         if (__all(c0.y == want && c0.w == want)) {
             bool ok = true;
             *dst[0] = make_float2(__uint_as_float(c0.x), __uint_as_float(c0.z));
@@ -197,6 +200,7 @@ __device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M]
             }
             if (__all(ok)) return true;
         }
+        c0 = c1;
         if ((++n & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
             if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
             return false;
