@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-end GPU pass: every bench line kept under profiles/, the GPU test suite and smoke(),
+# each under its own time limit; stops at the first crash or timeout.
+set -u
+O=gpurun_out/final
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+run() {  # run <name> <timeout> cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name" | tee -a $O/steps.log
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $O/steps.log
+  if [ $rc -ne 0 ]; then tail -8 "$O/$name.log"; echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+B="python bench.py --steps 3 --warmup 1 --cpu-seconds 0"
+S=${STEPS:-bench,mol,rr9,rr10,gen,c4,c4p,tests,smoke}
+[[ ,$S, == *,bench,* ]] && run bench 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 12
+[[ ,$S, == *,mol,* ]] && run mol 300 $B --mode MOL
+[[ ,$S, == *,rr9,* ]] && run rr9 300 $B --model runtimeracer-wavernn --bits 9
+[[ ,$S, == *,rr10,* ]] && run rr10 300 $B --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000
+[[ ,$S, == *,gen,* ]] && run gen 300 $B --model geneing-wavernn --mode BITS --bits 10
+[[ ,$S, == *,c4,* ]] && run c4 400 $B --utts-per-gpu 8
+[[ ,$S, == *,c4p,* ]] && run c4p 300 $B --utts-per-gpu 1 --frames 1700
+[[ ,$S, == *,tests,* ]] && run tests 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+[[ ,$S, == *,smoke,* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+exit 0
