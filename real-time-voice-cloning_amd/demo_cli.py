@@ -64,6 +64,11 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--out-dir", default=None, help="write demo_output_XX.wav files here")
     ap.add_argument("--vocoder-type", default="fatchord-wavernn")
+    ap.add_argument("--repeat", type=int, default=2,
+                    help="timed passes over the same utterances; the last one is reported")
+    ap.add_argument("--warmup", type=int, default=1,
+                    help="untimed passes of a short utterance through the three models first "
+                         "(library and kernel initialisation), as a serving process would")
     args = ap.parse_args()
 
     import torch
@@ -110,58 +115,77 @@ def main():
         syn = Synthesizer(args.syn_model_fpath, verbose=False, device=dev)
         vocoder.load_model(args.voc_model_fpath, device=local)
     syn.load()
-    if args.seed is not None:
-        torch.manual_seed(args.seed)
-        vocoder.set_seed(args.seed)
-        set_dropout_stream(args.seed)  # reproducible prenet dropout
+    for _ in range(args.warmup):
+        wv = encoder.preprocess_wav(synthetic_voice(seconds=1.0, seed=99), source_sr=16000)
+        syn.synthesize_spectrograms(["warm up"], [encoder.embed_utterance(wv)], steps=20)
+        mw = torch.zeros(sp.num_mels, 30, device=dev)  # >= 21 frames: the tail fade needs 20 hops
+        hw = hparams_for(vocoder.get_model().model_type)
+        vocoder.get_model().generate_batch([mw], True, hw.gen_target, hw.gen_overlap, hw.mu_law,
+                                           sp.preemphasize)
     t_load = time.perf_counter() - t0
 
     mine = [i for i in range(args.utterances) if i % world == rank]
     texts = [TEXTS[i % len(TEXTS)] for i in mine]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    # 1. speaker embedding of the reference utterance
-    if args.ref_wav:
-        ref = encoder.preprocess_wav(args.ref_wav)
-    else:
-        ref = encoder.preprocess_wav(synthetic_voice(seed=args.seed or 0), source_sr=16000)
-    embed = encoder.embed_utterance(ref)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    # 2. spectrograms for this rank's texts (one Tacotron batch)
-    specs = syn.synthesize_spectrograms(texts, [embed] * len(texts), steps=args.max_frames) if texts else []
-    torch.cuda.synchronize(dev)
-    t2 = time.perf_counter()
-    # 3. vocoder: all of this rank's mels as one batch of fold rows (infer_waveform semantics)
-    wavs = []
-    if specs:
-        model = vocoder.get_model()
-        hpv = hparams_for(model.model_type)
-        mels = [torch.from_numpy(np.ascontiguousarray(s / sp.max_abs_value, dtype=np.float32)).to(dev)
-                for s in specs]
-        wavs = model.generate_batch(mels, True, hpv.gen_target, hpv.gen_overlap, hpv.mu_law,
-                                    sp.preemphasize)
-    torch.cuda.synchronize(dev)
-    t3 = time.perf_counter()
-    # 4. post: pad 1 s (demo_cli.py:197), trim / normalise like the reference
-    outs = [encoder.preprocess_wav(np.pad(w, (0, sp.sample_rate), mode="constant").astype(np.float32))
-            for w in wavs]
-    t4 = time.perf_counter()
+
+    def run_pass():
+        if args.seed is not None:
+            torch.manual_seed(args.seed)
+            vocoder.set_seed(args.seed)
+            set_dropout_stream(args.seed)  # reproducible prenet dropout
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        # 1. speaker embedding of the reference utterance
+        if args.ref_wav:
+            ref = encoder.preprocess_wav(args.ref_wav)
+        else:
+            ref = encoder.preprocess_wav(synthetic_voice(seed=args.seed or 0), source_sr=16000)
+        embed = encoder.embed_utterance(ref)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        # 2. spectrograms for this rank's texts (one Tacotron batch)
+        specs = syn.synthesize_spectrograms(texts, [embed] * len(texts), steps=args.max_frames) if texts else []
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        # 3. vocoder: all of this rank's mels as one batch of fold rows (infer_waveform semantics)
+        wavs = []
+        if specs:
+            model = vocoder.get_model()
+            hpv = hparams_for(model.model_type)
+            mels = [torch.from_numpy(np.ascontiguousarray(s / sp.max_abs_value, dtype=np.float32)).to(dev)
+                    for s in specs]
+            wavs = model.generate_batch(mels, True, hpv.gen_target, hpv.gen_overlap, hpv.mu_law,
+                                        sp.preemphasize)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        # 4. post: pad 1 s (demo_cli.py:197), trim / normalise like the reference
+        outs = [encoder.preprocess_wav(np.pad(w, (0, sp.sample_rate), mode="constant").astype(np.float32))
+                for w in wavs]
+        t4 = time.perf_counter()
+        return np.array([t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0]), specs, wavs, outs
+
+    # The same pass twice by default: the first pays the libraries' first use of every new
+    # shape (MIOpen kernels of the encoder / Tacotron convolutions and GRUs; no cache persists
+    # on a fresh box), the last is the steady state reported.
+    totals = []
+    for _ in range(max(1, args.repeat)):
+        st, specs, wavs, outs = run_pass()
+        totals.append(st[4])
     if args.out_dir:
         from scipy.io import wavfile
         os.makedirs(args.out_dir, exist_ok=True)
         for i, w in zip(mine, outs):
             wavfile.write(os.path.join(args.out_dir, "demo_output_%02d.wav" % i), sp.sample_rate,
                           w.astype(np.float32))
-    stages = np.array([t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0, float(sum(len(w) for w in wavs))])
+    stages = np.concatenate([st, [float(sum(len(w) for w in wavs))], [totals[0]]])
     if world > 1:
-        ts = torch.tensor(stages[:5], device=red_dev, dtype=torch.float64)
+        ts = torch.tensor(stages[[0, 1, 2, 3, 4, 6]], device=red_dev, dtype=torch.float64)
         dist.all_reduce(ts, op=dist.ReduceOp.MAX)
         n = torch.tensor([stages[5]], device=red_dev, dtype=torch.float64)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        stages = np.concatenate([ts.cpu().numpy(), n.cpu().numpy()])
+        t_ = ts.cpu().numpy()
+        stages = np.concatenate([t_[:5], n.cpu().numpy(), t_[5:]])
     if rank == 0:
         audio_s = stages[5] / sp.sample_rate
         print(json.dumps({
@@ -169,6 +193,8 @@ def main():
             "utterances": args.utterances, "weights": "random(seed=%s)" % rw if rw is not None else "checkpoints",
             "vocoder": vocoder.get_model().model_type, "vocoder_engine": vocoder.get_model().last_engine(),
             "mel_frames": [int(s.shape[1]) for s in specs], "audio_seconds": round(audio_s, 3),
+            "warmup_passes": args.warmup, "passes": max(1, args.repeat),
+            "first_pass_total_seconds": round(stages[6], 4),
             "seconds": {"load": round(t_load, 3), "encoder": round(stages[0], 4),
                         "synthesizer": round(stages[1], 4), "vocoder": round(stages[2], 4),
                         "post": round(stages[3], 4), "total": round(stages[4], 4)},

@@ -48,6 +48,20 @@ def prenet_dropout(x, p):
     return F.dropout(x, p, training=True)
 
 
+class _StaticMasks:
+    """Prenet dropout inside a captured decoder chunk: call i multiplies by slot i of a device
+    buffer that is refilled (from the mask stream) before every replay."""
+
+    def __init__(self, buf):
+        self.buf = buf  # list of (B, dims) tensors, in call order
+        self.i = 0
+
+    def __call__(self, x, p):
+        m = self.buf[self.i]
+        self.i += 1
+        return x * m
+
+
 class BatchNormConv(nn.Module):
     """conv (no bias, 'same' padding) -> optional ReLU -> BatchNorm (common_layers.py:38-50)."""
 
@@ -176,8 +190,9 @@ class Decoder(nn.Module):
         self.mel_proj = nn.Linear(lstm_dims, n_mels * self.max_r, bias=False)
         self.stop_proj = nn.Linear(encoder_dims + spk_dims + lstm_dims, 1)
 
-    def forward(self, enc, enc_proj, prenet_in, state, context, t, chars):
-        """One decoder iteration (tacotron.py:244-299, eval mode: no zoneout)."""
+    def forward(self, enc, enc_proj, prenet_in, state, context, t, chars, r=None):
+        """One decoder iteration (tacotron.py:244-299, eval mode: no zoneout). ``r``: the
+        reduction factor as a host int (read from the buffer when absent)."""
         attn_h, h1, h2, c1, c2 = state
         attn_in = torch.cat([context, self.prenet(prenet_in)], dim=-1)
         attn_h = self.attn_rnn(attn_in.squeeze(1), attn_h)
@@ -188,7 +203,8 @@ class Decoder(nn.Module):
         x = x + h1
         h2, c2 = self.res_rnn2(x, (h2, c2))
         x = x + h2
-        mels = self.mel_proj(x).view(x.size(0), self.n_mels, self.max_r)[:, :, :int(self.r)]
+        r = int(self.r) if r is None else r
+        mels = self.mel_proj(x).view(x.size(0), self.n_mels, self.max_r)[:, :, :r]
         stop = torch.sigmoid(self.stop_proj(torch.cat((x, context), dim=1)))
         return mels, scores, (attn_h, h1, h2, c1, c2), context, stop
 
@@ -229,9 +245,19 @@ class Tacotron(nn.Module):
         self.load_state_dict(checkpoint["model_state"])
 
     @torch.no_grad()
-    def generate(self, x, speaker_embedding=None, steps=2000):
-        """tacotron.py:393-450: returns (mel_outputs, postnet linear (B, fft_bins, T), attention)."""
+    def generate(self, x, speaker_embedding=None, steps=2000, graph=None):
+        """tacotron.py:393-450: returns (mel_outputs, postnet linear (B, fft_bins, T), attention).
+
+        ``graph`` (default: on a GPU): run the decoder loop as replays of a captured HIP graph of
+        ``GRAPH_CHUNK`` iterations (the eager loop is launch-bound: ~30 small kernels per
+        iteration). Same kernels in the same order as the eager loop, same masks (the dropout
+        stream is advanced exactly as the eager loop would), same stop rule: the outputs equal
+        the eager ones."""
         self.eval()
+        if graph is None:
+            graph = x.is_cuda
+        if graph:
+            return self._generate_graph(x, speaker_embedding, steps)
         dev = next(self.parameters()).device
         B = x.size(0)
         z = lambda n: torch.zeros(B, n, device=dev)  # noqa: E731
@@ -250,6 +276,100 @@ class Tacotron(nn.Module):
             prenet_in = mels[:, :, -1]
             if (stop > 0.5).all() and t > 10:
                 break
+        mel_outputs = torch.cat(mel_outputs, dim=2)
+        linear = self.post_proj(self.postnet(mel_outputs)).transpose(1, 2)
+        return mel_outputs, linear, torch.cat(attn, 1)
+
+    GRAPH_CHUNK = 32
+
+    def _generate_graph(self, x, speaker_embedding, steps):
+        global _dropout
+        dev = x.device
+        B, r, C = x.size(0), self.r, self.GRAPH_CHUNK
+        dec = self.decoder
+        z = lambda n: torch.zeros(B, n, device=dev)  # noqa: E731
+        enc = self.encoder(x, speaker_embedding)  # (eager: consumes the encoder's mask calls)
+        enc_proj = self.encoder_proj(enc)
+        # static inputs / carried state of the captured chunk
+        st = [z(self.decoder_dims), z(self.lstm_dims), z(self.lstm_dims), z(self.lstm_dims),
+              z(self.lstm_dims)]
+        context = z(self.encoder_dims + self.speaker_embedding_size)
+        prenet_in = z(self.n_mels)
+        cum = torch.zeros(B, enc_proj.size(1), device=dev)
+        d1, d2 = dec.prenet.fc1.out_features, dec.prenet.fc2.out_features
+        stream = _dropout
+        flat = torch.empty(C * B * (d1 + d2), device=dev)  # one copy per replay
+        sizes = [B * d for _ in range(C) for d in (d1, d2)]
+        masks = [v.view(B, -1) for v in torch.split(flat, sizes)]
+        hist_m = torch.empty(C, B, self.n_mels, r, device=dev)
+        hist_s = torch.empty(C, B, 1, enc_proj.size(1), device=dev)
+        hist_stop = torch.empty(C, B, 1, device=dev)
+
+        def chunk():
+            state = tuple(st)
+            ctx, pin = context, prenet_in
+            dec.attn_net.cumulative = cum
+            for i in range(C):
+                mels, scores, state, ctx, stop = dec(enc, enc_proj, pin, state, ctx, 1, x, r)
+                hist_m[i].copy_(mels)
+                hist_s[i].copy_(scores)
+                hist_stop[i].copy_(stop)
+                pin = mels[:, :, -1]
+            for a, b in zip(st, state):
+                a.copy_(b)
+            context.copy_(ctx)
+            prenet_in.copy_(pin)
+            cum.copy_(dec.attn_net.cumulative)
+
+        def fill_masks(base):  # the stream's calls base.. of this chunk, in the eager order
+            host = np.empty(flat.numel(), np.float32)
+            o = 0
+            for k, m in enumerate(masks):
+                rng = np.random.Generator(np.random.PCG64([stream.seed, base + k]))
+                keep = (rng.random(tuple(m.shape)) >= dec.prenet.p).astype(np.float32)
+                host[o:o + m.numel()] = (keep / (1.0 - dec.prenet.p)).ravel()
+                o += m.numel()
+            flat.copy_(torch.from_numpy(host))
+
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        saved = [t.clone() for t in st] + [context.clone(), prenet_in.clone(), cum.clone()]
+        try:
+            if stream is not None:
+                _dropout = _StaticMasks(masks)
+            with torch.cuda.stream(side):  # warm-up (allocations, library handles), then capture
+                if stream is not None:
+                    _dropout.i = 0
+                chunk()
+                if stream is not None:
+                    _dropout.i = 0
+                with torch.cuda.graph(g, stream=side):
+                    chunk()
+        finally:
+            _dropout = stream
+        torch.cuda.current_stream(dev).wait_stream(side)
+        for t_, s_ in zip(st + [context, prenet_in, cum], saved):  # undo the warm-up chunk
+            t_.copy_(s_)
+        base = stream.calls if stream is not None else 0
+        mel_outputs, attn = [], []
+        done = 0
+        for t0 in range(0, steps, C * r):
+            if stream is not None:
+                fill_masks(base + 2 * (t0 // r))
+            g.replay()
+            n = min(C, (steps - t0 + r - 1) // r)
+            stops = (hist_stop[:n] > 0.5).all(dim=2).all(dim=1).cpu().numpy()
+            ts = t0 + r * np.arange(n)
+            hit = np.nonzero(stops & (ts > 10))[0]
+            k = int(hit[0]) + 1 if len(hit) else n
+            mel_outputs.extend(hist_m[i].clone() for i in range(k))
+            attn.extend(hist_s[i].clone() for i in range(k))
+            done += k
+            if len(hit) or k < C:
+                break
+        if stream is not None:
+            stream.calls = base + 2 * done
         mel_outputs = torch.cat(mel_outputs, dim=2)
         linear = self.post_proj(self.postnet(mel_outputs)).transpose(1, 2)
         return mel_outputs, linear, torch.cat(attn, 1)
