@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // loads of a batch in flight together (one LDS round trip per batch, not per row);
         // each row still accumulates in k order, as a row-outer loop would.
         auto mv3 = [&](const float4* Xs, float& s0, float& s1, float& s2) {
-            constexpr int QB = WRNN_PQB3;
+            constexpr int QB = NR >= 4 ? 1 : WRNN_PQB3;
             v2f acc[NR][3];
 #pragma unroll
             for (int r = 0; r < NR; ++r)
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         PSTAMP(2);
         // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
         auto mv1 = [&](float bias) {
-            constexpr int QB = WRNN_PQB1;
+            constexpr int QB = NR >= 4 ? 1 : WRNN_PQB1;
             float s0 = 0.f;
             v2f acc[NR];
 #pragma unroll
@@ -821,21 +821,22 @@ int persist_spill_t() {
     return (int)fa.localSizeBytes;
 }
 
-// 1 when the (rows per group, classes per slot) variant exists and keeps its state in
-// registers (no scratch spills: scratch traffic would serialise behind every exchange).
-int persist_variant_ok(int nr, int cpw) {
-    if (cpw < 1 || cpw > kPCls) return 0;
+// Scratch bytes of the (rows per group, classes per slot) variant; -1 when it does not exist.
+int persist_variant_scratch(int nr, int cpw) {
+    if (cpw < 1 || cpw > kPCls) return -1;
     const bool r = cpw > 16;
-    int sp = -1;
     switch (nr) {
-        case 1: sp = r ? persist_spill_t<1, true>() : persist_spill_t<1, false>(); break;
-        case 2: sp = r ? persist_spill_t<2, true>() : persist_spill_t<2, false>(); break;
-        case 3: sp = r ? persist_spill_t<3, true>() : persist_spill_t<3, false>(); break;
-        case 4: sp = r ? persist_spill_t<4, true>() : persist_spill_t<4, false>(); break;
-        default: break;
+        case 1: return r ? persist_spill_t<1, true>() : persist_spill_t<1, false>();
+        case 2: return r ? persist_spill_t<2, true>() : persist_spill_t<2, false>();
+        case 3: return r ? persist_spill_t<3, true>() : persist_spill_t<3, false>();
+        case 4: return r ? persist_spill_t<4, true>() : persist_spill_t<4, false>();
+        default: return -1;
     }
-    return sp == 0 ? 1 : 0;
 }
+
+// 1 when the variant exists and keeps its state in registers (no scratch spills: scratch
+// traffic would serialise behind every exchange).
+int persist_variant_ok(int nr, int cpw) { return persist_variant_scratch(nr, cpw) == 0 ? 1 : 0; }
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)

@@ -1721,6 +1721,16 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 : h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw)
                            : persist_variant_ok(r, h->pw.cpw))
                 nr_max = r;
+    // fatchord at 9 bits: 4 rows per group exist only with a few spilled registers (9.5 us per
+    // step against 7.2 at 3 rows, MI355X); take them when fewer launches pay for it
+    // (30 rows: 1 launch at 9.5 us instead of 2 at 7.2; 144 rows: 6 x 7.2 beats 5 x 9.5)
+    if (h->pw.ok && !h->pw.gen && !h->pw.rr && nr_max == 3 && h->pw.cpw <= 16) {
+        const int sc = persist_variant_scratch(4, h->pw.cpw);
+        const int b3 = (B + kPG * 3 - 1) / (kPG * 3), b4 = (B + kPG * 4 - 1) / (kPG * 4);
+        if (sc > 0 && sc <= 64 && b4 * 9.5 < b3 * 7.2) nr_max = 4;
+    }
+    if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX"))  // diagnostic: variant A/B
+        if (h->pw.ok) nr_max = std::max(1, std::min(kPNR, std::atoi(env)));
     const int nbatch = nr_max ? (B + kPG * nr_max - 1) / (kPG * nr_max) : 0;
     const int nr = nbatch ? (B + kPG * nbatch - 1) / (kPG * nbatch) : 0;
     bool use_p = false;
