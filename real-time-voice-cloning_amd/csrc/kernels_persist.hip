@@ -10,7 +10,8 @@
 // (r,z,n rows of the slot's units) and the fc1/fc2 rows; LDS holds the W_hh2 rows and the fc3
 // rows (registers when a slot owns more than 16 classes, i.e. 10-bit). Nothing is re-read from
 // HBM per step except the precomputed per-step inputs (P1, cI, per-frame aux terms, Gumbel
-// noise), all issued at the top of the step so their latency hides behind the exchanges.
+// noise), loaded a step ahead so their latency hides behind the exchanges (an explicit L2
+// warm-up two steps ahead measured 5 % slower and was dropped).
 //
 // Per step, four in-group exchanges of tagged pairs (value, step + 1) stored to the group's
 // exchange area and polled with non-temporal loads served by the XCD's shared L2:
@@ -56,8 +57,7 @@ constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's ro
 constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
 constexpr int L_W0 = L_BIAS + 96;                    // w0 = W_ih1[:, 0] [512] (GRU1 input term)
 constexpr int L_BCLS = L_W0 + kPH;                  // b_fc3 of the slot's classes [32]
-constexpr int L_SCR = L_BCLS + kPCls;               // landing line of the L2 warm-up loads [64]
-constexpr int L_W = (L_SCR + 64 + 3) & ~3;          // slot weights (kPLdsW4 float4)
+constexpr int L_W = (L_BCLS + kPCls + 3) & ~3;      // slot weights (kPLdsW4 float4)
 constexpr int L_FC3 = L_W + 16 * 3 * kPH;           // fc3 rows inside the weight block
 constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
@@ -218,34 +218,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pgn = bld(mk_rsrc(a.gumbel + (size_t)te * a.B * a.n_classes), o_gum, 0);
         }
     };
-    // L2 warm-up of step tt's streamed inputs (P1, cI, Gumbel rows of this group), one line
-    // per load, spread over the group's 32 workgroups; issued by waves 4-7 after their
-    // publish so no exchange waits on them.
-    const int lines_g = a.mode == 0 ? a.n_classes / 32 : 1;
-    const int lines_r = 48 + 16 + lines_g;
-    // (LDS-DMA loads into a scratch line: the warm-up holds no register and nothing waits on it)
-    auto touch = [&](int tt) {
-        const int i = tid - 256;
-        const int li = w + kPM * i;
-        if (tt >= a.S || i < 0 || li >= NR * lines_r) return;
-        const int r = li / lines_r, l = li % lines_r, row = g0 + kPG * r;
-        float* scr = lds + L_SCR;
-        if (l < 48)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.P1 + (size_t)tt * a.B * 3 * H), scr, 4,
-                                                     (unsigned)(row * 3 * H + l * 32) * 4u, 0, 0, 0);
-        else if (l < 64)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.cI + (size_t)tt * a.B * H), scr, 4,
-                                                     (unsigned)(row * H + (l - 48) * 32) * 4u, 0, 0, 0);
-        else {
-            const int gw = a.mode == 0 ? a.n_classes : kMolNoise;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(mk_rsrc(a.gumbel + (size_t)tt * a.B * gw), scr, 4,
-                                                     (unsigned)(row * gw + (l - 64) * 32) * 4u, 0, 0, 0);
-        }
-    };
     if (tid == 0) lds[L_FAIL] = 0.f;
     prefetch(a.t0, a.t0);
     pgum = pgn;
-    touch(a.t0 + 1);
     __syncthreads();
     const int tl = tid & 255;  // index inside the half that stages
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
@@ -365,7 +340,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             // gh1 (hop A) must be in L2 before this wave's y1 can be seen
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
-            touch(t + 2);
         }
         // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path, spread over the
         // exchange waits: rows r % 3 == 0 by waves 0-3 in hop B, r % 3 == 1 by waves 4-7 in hop
