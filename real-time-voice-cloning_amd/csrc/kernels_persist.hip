@@ -42,7 +42,9 @@ constexpr int XB_C = XB_B + kPNR * kPH * 2;
 constexpr int XB_D = XB_C + kPNR * kPH * 2;
 constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][value, tag]
 constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
-constexpr int XB_GROUP = XB_D + XB_D_SZ + 64;
+constexpr int XB_G = XB_D + XB_D_SZ;              // gh1 [parity][r][unit] (r, z, n, -) float4
+constexpr int XB_G_SZ = 2 * kPNR * kPH * 4;
+constexpr int XB_GROUP = XB_G + XB_G_SZ + 64;
 
 // LDS carve (floats). The per-step operands come first so every ds_read offset of the inner
 // loops fits the 16-bit immediate (no per-(q, row) address registers).
@@ -188,16 +190,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // unused): every path to the loop's back edge then consumes them, so the compiler's
     // wait insertion sees no load pending at the top of the step.
     auto prefetch = [&](int tg, int te) {
-        {
+        {  // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
             const int tn = tg + 1 < a.S ? tg + 1 : a.S - 1;
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * H);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * H);
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 4 * H);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    pP[r][j] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * H + j * H) * 4u);
-                pC[r] = bld(cr, o_tid, (unsigned)(r * kPG * H) * 4u);
+                const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, o_tid * 4u,
+                                                                     (unsigned)(r * kPG * 4 * H) * 4u, 0);
+                pP[r][0] = __uint_as_float(v.x);
+                pP[r][1] = __uint_as_float(v.y);
+                pP[r][2] = __uint_as_float(v.z);
+                pC[r] = __uint_as_float(v.w);
             }
         }
         te = te < a.S ? te : a.S - 1;
@@ -282,11 +285,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     h2r = hn;
                     bst_tag(p_add(lds[L_X0 + lr * kPH + u], hn), seq, xr, o_u, sA);  // x2 = x1 + h2
                     bst_tag(hn, seq, xr, o_u, sA + kPH * 8);
-                } else {  // gh1 for GRU1 at the end of this step
+                } else {  // gh1 (r, z, n) of (row lr, unit u) for GRU1 at the end of this step
                     const float* b = lds + L_BIAS + (og - 16);  // b_hh1 of unit u
-                    bst_tag(p_add(s0, b[0]), seq, xr, o_u, sA + 2 * kPH * 8);
-                    bst_tag(p_add(s1, b[16]), seq, xr, o_u, sA + 3 * kPH * 8);
-                    bst_tag(p_add(s2, b[32]), seq, xr, o_u, sA + 4 * kPH * 8);
+                    const u4v v = {__float_as_uint(p_add(s0, b[0])), __float_as_uint(p_add(s1, b[16])),
+                                   __float_as_uint(p_add(s2, b[32])), 0u};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        v, xr, (unsigned)((((t & 1) * kPNR + lr) * kPH + u) * 4) * 4u, XB_G * 4, 0);
                 }
             }
         }
@@ -436,11 +440,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             // gh1 (stage A) was drained by its producer waves before they stored y1 (stage B),
             // and this workgroup has seen every slot's y1 tag (stage C staging): plain loads
 #pragma unroll
-            for (int r = 0; r < NR; ++r)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    pG[r][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                        xr, o_tid * 2u, sA + (unsigned)((r * 5 + 2 + j) * kPH) * 8u, kCpNT));
+            for (int r = 0; r < NR; ++r) {
+                const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+                    xr, o_tid * 4u, (unsigned)(XB_G + ((t & 1) * kPNR + r) * kPH * 4) * 4u, kCpNT);
+                pG[r][0] = __uint_as_float(v.x);
+                pG[r][1] = __uint_as_float(v.y);
+                pG[r][2] = __uint_as_float(v.z);
+            }
             prefetch(t, t + 1);  // pgn, not pgum: the fc3 epilogue still reads pgum
         };
 
@@ -687,11 +693,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
 // Step-0 state: GRU1 with x = 0, h = 0, gh = b_hh1 -> x1(0), h1(0); h2 = 0, gh2 = b_hh2.
 __global__ __launch_bounds__(kPT) void k_persist_init(PersistArgs a) {
     const int row = blockIdx.x, j = threadIdx.x, H = kPH;
-    const float* P1 = a.P1 + (size_t)row * 3 * H;  // step 0
-    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
-                           a.b_hh1[2 * H + j], 0.f);
+    const float* P1 = a.P1 + ((size_t)row * H + j) * 4;  // step 0: (r, z, n, cI) of unit j
+    const float hn = p_gru(P1[0], P1[1], P1[2], a.b_hh1[j], a.b_hh1[H + j], a.b_hh1[2 * H + j], 0.f);
     a.st_h1[(size_t)row * H + j] = hn;
-    a.st_x1[(size_t)row * H + j] = p_add(a.cI[(size_t)row * H + j], hn);
+    a.st_x1[(size_t)row * H + j] = p_add(P1[3], hn);
     a.st_h2[(size_t)row * H + j] = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) a.st_gh2[(size_t)row * 3 * H + k * H + j] = a.b_hh2[k * H + j];

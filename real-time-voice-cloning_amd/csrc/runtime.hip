@@ -176,6 +176,7 @@ struct wrnn_handle {
         int cpw = 0, nw = 0, oG2 = 0, oF1 = 0, oF2 = 0;  // rr: oG2 = oG3, oF2 = oF3
         const float *wreg = nullptr, *wlds = nullptr;
         const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
+        bool p1x4 = false;  // fatchord: P1 as [step][row][unit][r, z, n, cI] (one 16-B load)
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
@@ -348,7 +349,7 @@ std::vector<float> transpose_cols(const std::vector<float>& W, int rows, int ld,
 // P1 = W_ih1 (I[:,1:] c + b_I) + b_ih1 = M1 c + bP1 with M1 = W_ih1 I[:,1:] (f64 products):
 // one K = feat + A - 1 contraction per (step, row) instead of K = rnn_dims (both topologies
 // feed rnn1 with I(x0), fatchord_version.py:198-201, runtimeracer_version.py:248-252)
-int pack_p1(wrnn_handle* h) {
+int pack_p1(wrnn_handle* h, bool x4) {
     auto& T = h->host;
     auto& P = h->pw;
     const int H = h->H, A = h->A;
@@ -375,6 +376,22 @@ int pack_p1(wrnn_handle* h) {
             }
             for (int k = 0; k < KI; ++k) M1T[(size_t)k * 3 * H + o] = (float)acc[k];
             bP1[o] = (float)b;
+        }
+        P.p1x4 = x4;
+        if (x4) {  // columns unit-major, 4 per unit: gates r, z, n of P1, then cI (I.weight)
+            std::vector<float> M4((size_t)KI * 4 * H), b4(4 * H);
+            for (int k = 0; k < KI; ++k)
+                for (int j = 0; j < H; ++j) {
+                    for (int g = 0; g < 3; ++g)
+                        M4[(size_t)k * 4 * H + 4 * j + g] = M1T[(size_t)k * 3 * H + g * H + j];
+                    M4[(size_t)k * 4 * H + 4 * j + 3] = (float)WIk[(size_t)j * KI + k];
+                }
+            for (int j = 0; j < H; ++j) {
+                for (int g = 0; g < 3; ++g) b4[4 * j + g] = bP1[g * H + j];
+                b4[4 * j + 3] = bI[j];
+            }
+            M1T.swap(M4);
+            bP1.swap(b4);
         }
         P.M1T = upload(h, M1T, &rc);
         CHECK(rc);
@@ -442,7 +459,7 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     CHECK(rc);
     P.wlds = upload(h, wlds, &rc);
     CHECK(rc);
-    CHECK(pack_p1(h));
+    CHECK(pack_p1(h, true));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
@@ -511,7 +528,7 @@ int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
     CHECK(rc);
     P.wlds = upload(h, w5, &rc);
     CHECK(rc);
-    CHECK(pack_p1(h));
+    CHECK(pack_p1(h, false));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
@@ -574,7 +591,7 @@ int pack_persist_gen(wrnn_handle* h, int oF1) {
     P.wreg = upload(h, wreg, &rc);
     CHECK(rc);
     P.wlds = nullptr;
-    CHECK(pack_p1(h));
+    CHECK(pack_p1(h, false));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
@@ -1038,12 +1055,13 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         e4.row0 = row0;
         HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
         if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
+            const int np = h->pw.p1x4 ? 4 * H : 3 * H;  // (fatchord: + cI, unit-major)
             b4.p = h->pw.M1T;
-            b4.ld = 3 * H;
+            b4.ld = np;
             e4.D = P1out;
-            e4.ld = 3 * H;
+            e4.ld = np;
             e4.bias = h->pw.bP1;
-            HIPC(launch_gemm(S * Bu, 3 * H, h->KI, a4, b4, e4, st));
+            HIPC(launch_gemm(S * Bu, np, h->KI, a4, b4, e4, st));
         }
     }
     // per-frame aux conditioning, slot 0 = zero frame
@@ -1780,7 +1798,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
                         hipMemcpyHostToDevice, h->stream));
     // upsample + conditioning per utterance (cI folded with row stride Bp)
-    if (use_p) CHECK(h->pws.P1.alloc((size_t)S * Bp * 3 * kPH * sizeof(float)));
+    if (use_p) CHECK(h->pws.P1.alloc((size_t)S * Bp * (h->pw.p1x4 ? 4 : 3) * kPH * sizeof(float)));
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
                            plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr));
