@@ -274,6 +274,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         };
         // ================= stage A: GRU2 (waves 0-3, critical) | W_hh1 h1 + b -> gh1 (4-7) ====
         {
+            // GRU2 waves first on each SIMD (a W_hh1 wave shares it; gh1 is needed only at GRU1)
+            if (gate_a) __builtin_amdgcn_s_setprio(2);
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             mv3(gate_a ? X0 : X1, s0, s1, s2);
             XSTAMP(29);
@@ -294,6 +296,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 }
             }
         }
+        __builtin_amdgcn_s_setprio(0);
         XSTAMP(30);
         PSTAMP(1);
         // ===== hop A: stage x2 -> X0, h2 -> XH2 (waves 0-3) ======================================

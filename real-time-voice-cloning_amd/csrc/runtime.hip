@@ -1739,13 +1739,14 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 : h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw)
                            : persist_variant_ok(r, h->pw.cpw))
                 nr_max = r;
-    // fatchord at 9 bits: 4 rows per group exist only with a few spilled registers (8.3 us per
-    // step against 6.7 at 3 rows, MI355X); take them when fewer launches pay for it
+    // fatchord at 9 bits: 4 rows per group cost 8.3 us per step against 6.7 at 3 rows (MI355X;
+    // the 4-row variant may also hold a few spilled registers): take them only when fewer
+    // launches pay for it
     // (30 rows: 1 launch at 8.3 us instead of 2 at 6.7; 144 rows: 6 x 6.7 beats 5 x 8.3)
-    if (h->pw.ok && !h->pw.gen && !h->pw.rr && nr_max == 3 && h->pw.cpw <= 16) {
+    if (h->pw.ok && !h->pw.gen && !h->pw.rr && nr_max >= 3 && h->pw.cpw <= 16) {
         const int sc = persist_variant_scratch(4, h->pw.cpw);
         const int b3 = (B + kPG * 3 - 1) / (kPG * 3), b4 = (B + kPG * 4 - 1) / (kPG * 4);
-        if (sc > 0 && sc <= 64 && b4 * 8.3 < b3 * 6.7) nr_max = 4;
+        nr_max = sc >= 0 && sc <= 64 && b4 * 8.3 < b3 * 6.7 ? 4 : 3;
     }
     if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX"))  // diagnostic: variant A/B
         if (h->pw.ok) nr_max = std::max(1, std::min(kPNR, std::atoi(env)));
