@@ -45,8 +45,8 @@ constexpr int RX_G = 0;                                    // GRU hops [3][kRNR]
 constexpr int RX_G_SZ = kRNR * 2 * RH * 2;
 constexpr int RX_F = RX_G + 3 * RX_G_SZ;                   // fc hops [4][kRNR][RH] pairs
 constexpr int RX_F_SZ = kRNR * RH * 2;
-constexpr int RX_GH1 = RX_F + 4 * RX_F_SZ;                 // gh1 [2 parity][kRNR][3 RH] floats
-constexpr int RX_GH1_SZ = kRNR * 3 * RH;
+constexpr int RX_GH1 = RX_F + 4 * RX_F_SZ;                 // gh1 [2 parity][kRNR][RH] (r, z, n, -)
+constexpr int RX_GH1_SZ = kRNR * 4 * RH;
 constexpr int RX_D = RX_GH1 + 2 * RX_GH1_SZ;               // candidates [kPM][kRNR] pairs
 constexpr int RX_D_LOG = kPM * kRNR * 2;
 constexpr int RX_GROUP = RX_D + RX_D_LOG + kRNR * 32 + 64; // + MOL logits [kRNR][32]
@@ -302,12 +302,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         } else if (q == 1) {
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H1), kc, s0, s1, s2);
-            if (own) {
-                const unsigned o = (unsigned)((par * kRNR + kc) * 3 * RH + u) * 4u;
-                const unsigned so = (unsigned)RX_GH1 * 4u;
-                bst(p_add(s0, cb[CB_HH1 + og]), xr, o, so);
-                bst(p_add(s1, cb[CB_HH1 + 8 + og]), xr, o + RH * 4, so);
-                bst(p_add(s2, cb[CB_HH1 + 16 + og]), xr, o + 2 * RH * 4, so);
+            if (own) {  // gh1 (r, z, n) of (row kc, unit u): one 16-byte store
+                const u4v v = {__float_as_uint(p_add(s0, cb[CB_HH1 + og])),
+                               __float_as_uint(p_add(s1, cb[CB_HH1 + 8 + og])),
+                               __float_as_uint(p_add(s2, cb[CB_HH1 + 16 + og])), 0u};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    v, xr, (unsigned)(((par * kRNR + kc) * RH + u) * 4) * 4u, (unsigned)RX_GH1 * 4u, 0);
             }
             // gh1 reaches L2 before this wave's later publishes (GRU4 at stage 3): a consumer
             // that has seen every slot's x4/h4 tags reads gh1 with plain loads
@@ -386,24 +386,28 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
 #pragma unroll
         for (int i = 0; i < NRH; ++i) {
             const int r = 2 * i + hs < NR ? 2 * i + hs : 0;
-#pragma unroll
-            for (int jg = 0; jg < 3; ++jg)
-                pG[i][jg] = bld_nt(xr, o_tid, (unsigned)(RX_GH1 + (par * kRNR + r) * 3 * RH + jg * RH) * 4u);
+            const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+                xr, o_tid * 4u, (unsigned)(RX_GH1 + (par * kRNR + r) * 4 * RH) * 4u, kCpNT);
+            pG[i][0] = __uint_as_float(v.x);
+            pG[i][1] = __uint_as_float(v.y);
+            pG[i][2] = __uint_as_float(v.z);
         }
         // P1 / cI of step t+1 for the same GRU1 (HBM latency hides behind stages 4-8)
         float pP[NRH][3], pC[NRH];
         {  // (unconditional, step clamped: every path to the back edge consumes these loads)
             const int tn = nxt ? t + 1 : t;
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * RH);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * RH);
+            // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 4 * RH);
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
                 if (r < NR) {
-#pragma unroll
-                    for (int jg = 0; jg < 3; ++jg)
-                        pP[i][jg] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * RH + jg * RH) * 4u);
-                    pC[i] = bld(cr, o_tid, (unsigned)(r * kPG * RH) * 4u);
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+                        pr, o_tid * 4u, (unsigned)(r * kPG * 4 * RH) * 4u, 0);
+                    pP[i][0] = __uint_as_float(v.x);
+                    pP[i][1] = __uint_as_float(v.y);
+                    pP[i][2] = __uint_as_float(v.z);
+                    pC[i] = __uint_as_float(v.w);
                 }
             }
         }
@@ -656,11 +660,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
 // gh2 = b_hh2, gh3 = b_hh3.
 __global__ __launch_bounds__(kRH) void k_persist_rr_init(PersistRRArgs a) {
     const int row = blockIdx.x, j = threadIdx.x, H = kRH;
-    const float* P1 = a.P1 + (size_t)row * 3 * H;  // step 0
-    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
+    const float* P1 = a.P1 + ((size_t)row * H + j) * 4;  // step 0: (r, z, n, cI) of unit j
+    const float hn = p_gru(P1[0], P1[1], P1[2], a.b_hh1[j], a.b_hh1[H + j],
                            a.b_hh1[2 * H + j], 0.f);
     float* st = a.st + (size_t)row * 11 * H;
-    st[j] = p_add(a.cI[(size_t)row * H + j], hn);
+    st[j] = p_add(P1[3], hn);
     st[H + j] = hn;
     st[2 * H + j] = 0.f;
     st[3 * H + j] = 0.f;

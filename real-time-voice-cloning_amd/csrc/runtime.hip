@@ -528,7 +528,7 @@ int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
     CHECK(rc);
     P.wlds = upload(h, w5, &rc);
     CHECK(rc);
-    CHECK(pack_p1(h, false));
+    CHECK(pack_p1(h, true));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
