@@ -180,16 +180,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
         float pP[NRH][3], pC[NRH];
         {  // (unconditional, step clamped: every path to the back edge consumes these loads)
             const int tn = nxt ? t + 1 : t;
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 3 * GH);
-            const rsrc_t cr = mk_rsrc(a.cI + ((size_t)tn * a.B + g0) * GH);
+            // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 4 * GH);
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
                 if (r < NR) {
-#pragma unroll
-                    for (int jg = 0; jg < 3; ++jg)
-                        pP[i][jg] = bld(pr, o_tid, (unsigned)(r * kPG * 3 * GH + jg * GH) * 4u);
-                    pC[i] = bld(cr, o_tid, (unsigned)(r * kPG * GH) * 4u);
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+                        pr, o_tid * 4u, (unsigned)(r * kPG * 4 * GH) * 4u, 0);
+                    pP[i][0] = __uint_as_float(v.x);
+                    pP[i][1] = __uint_as_float(v.y);
+                    pP[i][2] = __uint_as_float(v.z);
+                    pC[i] = __uint_as_float(v.w);
                 }
             }
         }
@@ -420,11 +422,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
 // Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0).
 __global__ __launch_bounds__(kRH) void k_persist_gen_init(PersistGenArgs a) {
     const int row = blockIdx.x, j = threadIdx.x, H = GH;
-    const float* P1 = a.P1 + (size_t)row * 3 * H;
-    const float hn = p_gru(P1[j], P1[H + j], P1[2 * H + j], a.b_hh1[j], a.b_hh1[H + j],
-                           a.b_hh1[2 * H + j], 0.f);
+    const float* P1 = a.P1 + ((size_t)row * H + j) * 4;  // step 0: (r, z, n, cI) of unit j
+    const float hn = p_gru(P1[0], P1[1], P1[2], a.b_hh1[j], a.b_hh1[H + j], a.b_hh1[2 * H + j], 0.f);
     float* st = a.st + (size_t)row * 2 * H;
-    st[j] = p_add(a.cI[(size_t)row * H + j], hn);
+    st[j] = p_add(P1[3], hn);
     st[H + j] = hn;
 }
 

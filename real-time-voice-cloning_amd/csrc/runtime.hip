@@ -591,7 +591,7 @@ int pack_persist_gen(wrnn_handle* h, int oF1) {
     P.wreg = upload(h, wreg, &rc);
     CHECK(rc);
     P.wlds = nullptr;
-    CHECK(pack_p1(h, false));
+    CHECK(pack_p1(h, true));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
