@@ -1739,14 +1739,25 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 : h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw)
                            : persist_variant_ok(r, h->pw.cpw))
                 nr_max = r;
-    // fatchord at 9 bits: 4 rows per group cost 8.3 us per step against 6.7 at 3 rows (MI355X;
-    // the 4-row variant may also hold a few spilled registers): take them only when fewer
-    // launches pay for it
-    // (30 rows: 1 launch at 8.3 us instead of 2 at 6.7; 144 rows: 6 x 6.7 beats 5 x 8.3)
-    if (h->pw.ok && !h->pw.gen && !h->pw.rr && nr_max >= 3 && h->pw.cpw <= 16) {
-        const int sc = persist_variant_scratch(4, h->pw.cpw);
-        const int b3 = (B + kPG * 3 - 1) / (kPG * 3), b4 = (B + kPG * 4 - 1) / (kPG * 4);
-        nr_max = sc >= 0 && sc <= 64 && b4 * 8.3 < b3 * 6.7 ? 4 : 3;
+    // fatchord: rows per group by launch cost. A launch with more rows per group runs each
+    // step slower (measured MI355X us per step below; the larger variants may also hold a few
+    // spilled registers), so more rows per launch pay only when they save launches:
+    // 9-bit 30 rows -> one launch at 4 rows, 144 rows -> six at 3; 10-bit 45 rows -> two at 3.
+    if (h->pw.ok && !h->pw.gen && !h->pw.rr) {
+        static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
+        const int wide = h->pw.cpw > 16 ? 1 : 0;
+        double best = 0;
+        nr_max = 0;
+        for (int c = 1; c <= kPNR; ++c) {
+            const int sc = persist_variant_scratch(c, h->pw.cpw);
+            if (sc < 0 || sc > 64) continue;
+            const int nb = (B + kPG * c - 1) / (kPG * c), n = (B + kPG * nb - 1) / (kPG * nb);
+            const double cost = nb * us[wide][n];
+            if (!nr_max || cost <= best) {
+                nr_max = c;
+                best = cost;
+            }
+        }
     }
     if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX"))  // diagnostic: variant A/B
         if (h->pw.ok) nr_max = std::max(1, std::min(kPNR, std::atoi(env)));

@@ -97,3 +97,22 @@ def test_unbatched_unequal_lengths_refused():
     with pytest.raises((ValueError, RuntimeError)):
         _device_rows(m, meta, [synth_mel(4, 7), synth_mel(6, 8)], False, meta['target'],
                      meta['overlap'])
+
+
+@pytest.mark.parametrize('n_utts', [4, 6])
+def test_fatchord_10bit_row_groups_match_oracle(n_utts):
+    """10-bit fatchord (32 classes per slot, fc3 rows held in registers) at 20 / 30 fold rows:
+    the 3- and 4-rows-per-group variants the launch-cost choice takes, every row against the
+    oracle."""
+    from wavernn_amd.synth import synth_mel
+    meta = dict(golden_case('fatchord_raw9_sharp_tiny')[0])
+    meta['bits'] = 10
+    m, hp, sd = make_model(meta)
+    m.set_engine('persist')
+    mels = [synth_mel(meta['n_frames'], 400 + u) for u in range(n_utts)]
+    lab, roff, S = _device_rows(m, meta, mels, True, meta['target'], meta['overlap'])
+    assert m.last_engine() == 'persist'
+    for u in range(n_utts):
+        ref = _oracle_rows(sd, hp, meta, mels[u], meta['target'], meta['overlap'], stream=u)
+        got = lab[roff[u]:roff[u + 1]]
+        assert np.array_equal(got, ref), f'utt {u}: {first_divergence(got, ref)}'
