@@ -63,16 +63,21 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
     e.D[(size_t)m * e.ld + n] = v;
 }
 
+// NT 64-wide column tiles per workgroup share one staged A tile (the gathered conditioning
+// rows are read once per k step, not once per column tile).
+template <int NT>
 __global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
                                                    GemmEp E) {
     __shared__ float As[16][64];
-    __shared__ float Bs[16][64];
+    __shared__ float Bs[16][64 * NT];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv & 1, wn = wv >> 1;
-    const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-    floatx16 acc;
+    const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * NT;
+    floatx16 acc[NT];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
     for (int k0 = 0; k0 < K; k0 += 16) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -80,33 +85,48 @@ __global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A,
             const int mm = e & 63, kk = e >> 6;
             const int m = m0 + mm, k = k0 + kk;
             As[kk][mm] = (m < M && k < K) ? load_a(A, m, k) : 0.f;
-            const int n = n0 + mm;
-            Bs[kk][mm] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4 * NT; ++i) {
+            const int e = tid + i * kThreads;
+            const int nn = e % (64 * NT), kk = e / (64 * NT);
+            const int n = n0 + nn, k = k0 + kk;
+            Bs[kk][nn] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
         }
         __syncthreads();
 #pragma unroll
         for (int kp = 0; kp < 8; ++kp) {
             const float av = As[2 * kp + (lane >> 5)][wm * 32 + (lane & 31)];
-            const float bv = Bs[2 * kp + (lane >> 5)][wn * 32 + (lane & 31)];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float bv = Bs[2 * kp + (lane >> 5)][64 * t + wn * 32 + (lane & 31)];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+            }
         }
         __syncthreads();
     }
     // C/D map (32x32, 16 regs): col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int i = 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
-        const int j = lane & 31;
-        const int m = m0 + wm * 32 + i, n = n0 + wn * 32 + j;
-        if (m < M && n < N) store_ep(E, m, n, acc[r]);
-    }
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int i = 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+            const int j = lane & 31;
+            const int m = m0 + wm * 32 + i, n = n0 + 64 * t + wn * 32 + j;
+            if (m < M && n < N) store_ep(E, m, n, acc[t][r]);
+        }
 }
 
 hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, const GemmEp& e,
                        hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    dim3 grid((M + 63) / 64, (N + 63) / 64);
-    hipLaunchKernelGGL(k_gemm, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    if (N >= 1024) {  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
+        dim3 grid((M + 63) / 64, (N + 255) / 256);
+        hipLaunchKernelGGL(k_gemm<4>, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    } else {
+        dim3 grid((M + 63) / 64, (N + 63) / 64);
+        hipLaunchKernelGGL(k_gemm<1>, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    }
     return hipGetLastError();
 }
 
