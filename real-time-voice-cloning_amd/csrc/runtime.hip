@@ -118,6 +118,11 @@ struct wrnn_handle {
     wrnn_config cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
+    // PERSIST: the noise is generated on a side stream while the upsample / conditioning
+    // GEMMs run on `stream` (independent inputs); the recurrence waits on noise_done
+    hipStream_t side = nullptr;
+    hipEvent_t rows_ready = nullptr, noise_done = nullptr;
+    bool noise_pending = false;
     int H = 0, F = 0, A = 0, C = 0, R = 0, n_classes = 0, feat = 0, hop = 0, n_gru = 0, KI = 0;
     int indent = 0;
     std::map<std::string, std::vector<int64_t>> expected;
@@ -197,6 +202,9 @@ struct wrnn_handle {
     ~wrnn_handle() {
         for (auto e : pev) (void)hipEventDestroy(e);
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        if (rows_ready) (void)hipEventDestroy(rows_ready);
+        if (noise_done) (void)hipEventDestroy(noise_done);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -1453,24 +1461,40 @@ void persist_phase_report(wrnn_handle* h, int t) {
 // PERSIST engine: P1 for all steps (one MFMA GEMM), Gumbel noise (RAW), step-0 state, then
 // the persistent recurrence in chunks (one chunk per call unless a progress callback wants
 // reports; every 1000 steps then).
+// Gumbel (RAW) / MOL noise of every (step, row) of the call on stream `st` (the RNG contract).
+int persist_noise(wrnn_handle* h, int S, hipStream_t st) {
+    auto& P = h->pws;
+    const int Bp = h->last_Bp, n = h->n_classes;
+    const bool raw = h->cfg.mode == WRNN_MODE_RAW;
+    CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
+    const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
+    const RowInfo* rows = (const RowInfo*)h->ws.rows.p;
+    if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, rows, k0, k1, st));
+    else HIPC(launch_mol_noise(P.gumbel.f(), S, Bp, rows, k0, k1, st));
+    return WRNN_OK;
+}
+
 int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     auto& ws = h->ws;
     auto& P = h->pws;
     const auto& W = h->pw;
     const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;  // H: fatchord layout
-    const bool raw = h->cfg.mode == WRNN_MODE_RAW;
     hipStream_t st = h->stream;
-    CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
     CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
     const bool rr = W.rr, gen = W.gen;
     const size_t xfl = gen ? persist_gen_xbuf_floats() : rr ? persist_rr_xbuf_floats() : persist_xbuf_floats();
     CHECK(P.xbuf.alloc(xfl * sizeof(float)));
     CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? 11 * kRH : 6 * H) * sizeof(float)));
-    // P1 (all steps, rows) was written by run_upsample next to cI
+    // P1 (all steps, rows) was written by run_upsample next to cI; the noise by
+    // persist_noise on the side stream
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
-    if (raw) HIPC(launch_gumbel(P.gumbel.f(), S, Bp, n, (const RowInfo*)ws.rows.p, k0, k1, st));
-    else HIPC(launch_mol_noise(P.gumbel.f(), S, Bp, (const RowInfo*)ws.rows.p, k0, k1, st));
+    if (h->noise_pending) {
+        HIPC(hipStreamWaitEvent(st, h->noise_done, 0));
+        h->noise_pending = false;
+    } else {
+        CHECK(persist_noise(h, S, st));
+    }
     PersistArgs a{};
     a.ctl = (unsigned*)P.ctl.p;
     a.flags = (unsigned*)P.flags.p;
@@ -1811,6 +1835,18 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                         hipMemcpyHostToDevice, h->stream));
     // upsample + conditioning per utterance (cI folded with row stride Bp)
     if (use_p) CHECK(h->pws.P1.alloc((size_t)S * Bp * (h->pw.p1x4 ? 4 : 3) * kPH * sizeof(float)));
+    if (use_p) {  // noise on the side stream, concurrent with the upsample / conditioning GEMMs
+        if (!h->side) {
+            HIPC(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPC(hipEventCreateWithFlags(&h->rows_ready, hipEventDisableTiming));
+            HIPC(hipEventCreateWithFlags(&h->noise_done, hipEventDisableTiming));
+        }
+        HIPC(hipEventRecord(h->rows_ready, h->stream));
+        HIPC(hipStreamWaitEvent(h->side, h->rows_ready, 0));
+        CHECK(persist_noise(h, S, h->side));
+        HIPC(hipEventRecord(h->noise_done, h->side));
+        h->noise_pending = true;
+    }
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
                            plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr));
