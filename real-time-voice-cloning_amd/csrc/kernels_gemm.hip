@@ -13,21 +13,50 @@ namespace wrnn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float load_a(const GemmA& a, int m, int k) {
-    switch (a.kind) {
-        case 0:
-            return a.p[(size_t)m * a.ld + k];
-        case 1: {  // cI: [mel_up(p) (n_mel) | aux(p // hop)[r_off : r_off + n_aux]]
-            const int p = (m % a.Bu) * a.tpo + m / a.Bu;  // fold_with_overlap position
-            if (p >= a.L) return 0.f;                      // zero tail pad
-            if (k < a.n_mel) return a.mel[(size_t)k * a.ldm + p];
-            return a.R[(size_t)(a.r_off + k - a.n_mel) * a.ldr + p / a.hop];
-        }
-        default: {  // frame-A: slot 0 is the zero frame; slot f+1 = frame f
-            if (m == 0) return 0.f;
-            return a.R[(size_t)(a.r_off + k) * a.ldr + (m - 1)];
-        }
+// A(m, .) of one row as two strided segments: k < ksplit reads p0[o0 + k * s0], the rest
+// p1[o1 + k * s1] (o1 may be negative: it is only ever used with k >= ksplit). The row's
+// index math (the fold_with_overlap position, its frame) runs once per thread, not per k.
+struct ARow {
+    const float *p0, *p1;
+    long o0, o1;
+    int s0, s1, ksplit;
+    bool zero;
+};
+
+// AK = GemmA::kind as a template argument: one straight-line row setup per kernel (a runtime
+// switch over the kinds here was mis-structured by the compiler: the frame-A path lost p0).
+template <int AK>
+__device__ __forceinline__ ARow a_row(const GemmA& a, int m, int M) {
+    ARow r{};
+    r.zero = m >= M;
+    if constexpr (AK == 0) {
+        r.p0 = r.p1 = a.p;
+        r.o0 = r.o1 = (long)m * a.ld;
+        r.s0 = r.s1 = 1;
+        r.ksplit = 1 << 30;
+    } else if constexpr (AK == 1) {  // cI: [mel_up(p) (n_mel) | aux(p // hop)[r_off : r_off + n_aux]]
+        const int p = (m % a.Bu) * a.tpo + m / a.Bu;  // fold_with_overlap position
+        r.zero |= p >= a.L;                            // zero tail pad
+        r.p0 = a.mel;
+        r.o0 = p;
+        r.s0 = a.ldm;
+        r.p1 = a.R;
+        r.o1 = (long)(a.r_off - a.n_mel) * a.ldr + p / a.hop;
+        r.s1 = a.ldr;
+        r.ksplit = a.n_mel;
+    } else {  // frame-A: slot 0 is the zero frame; slot f+1 = frame f
+        r.zero |= m == 0;
+        r.p0 = r.p1 = a.R;
+        r.o0 = r.o1 = (long)a.r_off * a.ldr + (m - 1);
+        r.s0 = r.s1 = a.ldr;
+        r.ksplit = 1 << 30;
     }
+    return r;
+}
+
+__device__ __forceinline__ float load_a(const ARow& r, int k, int K) {
+    if (r.zero || k >= K) return 0.f;
+    return k < r.ksplit ? r.p0[r.o0 + (long)k * r.s0] : r.p1[r.o1 + (long)k * r.s1];
 }
 
 __device__ __forceinline__ float load_b(const GemmB& b, int k, int n) {
@@ -64,36 +93,45 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
 }
 
 // NT 64-wide column tiles per workgroup share one staged A tile (the gathered conditioning
-// rows are read once per k step, not once per column tile).
-template <int NT>
-__global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
+// rows are read once per k step, not once per column tile). The next k step's operands are
+// fetched into registers while the matrix cores work on the current one.
+template <int NT, int AK>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
                                                    GemmEp E) {
     __shared__ float As[16][64];
     __shared__ float Bs[16][64 * NT];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv & 1, wn = wv >> 1;
     const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * NT;
+    // this thread stages A(m0 + (tid & 63), k0 + (tid >> 6) + 4 i), i < 4
+    const ARow ar = a_row<AK>(A, m0 + (tid & 63), M);
+    float ra[4], rb[4 * NT];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[i] = load_a(ar, k0 + (tid >> 6) + 4 * i, K);
+#pragma unroll
+        for (int i = 0; i < 4 * NT; ++i) {
+            const int e = tid + i * kThreads;
+            const int n = n0 + e % (64 * NT), k = k0 + e / (64 * NT);
+            rb[i] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
+        }
+    };
     floatx16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    fetch(0);
     for (int k0 = 0; k0 < K; k0 += 16) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = tid + i * kThreads;
-            const int mm = e & 63, kk = e >> 6;
-            const int m = m0 + mm, k = k0 + kk;
-            As[kk][mm] = (m < M && k < K) ? load_a(A, m, k) : 0.f;
-        }
+        for (int i = 0; i < 4; ++i) As[(tid >> 6) + 4 * i][tid & 63] = ra[i];
 #pragma unroll
         for (int i = 0; i < 4 * NT; ++i) {
             const int e = tid + i * kThreads;
-            const int nn = e % (64 * NT), kk = e / (64 * NT);
-            const int n = n0 + nn, k = k0 + kk;
-            Bs[kk][nn] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
+            Bs[e / (64 * NT)][e % (64 * NT)] = rb[i];
         }
         __syncthreads();
+        if (k0 + 16 < K) fetch(k0 + 16);
 #pragma unroll
         for (int kp = 0; kp < 8; ++kp) {
             const float av = As[2 * kp + (lane >> 5)][wm * 32 + (lane & 31)];
@@ -106,6 +144,26 @@ __global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A,
         __syncthreads();
     }
     // C/D map (32x32, 16 regs): col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
+    if (E.kind == 3) {  // folded rows: the row index once per r, the bias once per tile
+        float bias[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n = n0 + 64 * t + wn * 32 + (lane & 31);
+            bias[t] = n < N ? E.bias[n] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+            if (m >= M) continue;
+            float* D = E.D + ((size_t)(m / E.Bu) * E.Btot + E.row0 + m % E.Bu) * E.ld;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int n = n0 + 64 * t + wn * 32 + (lane & 31);
+                if (n < N) D[n] = acc[t][r] + bias[t];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -117,16 +175,25 @@ __global__ __launch_bounds__(kThreads) void k_gemm(int M, int N, int K, GemmA A,
         }
 }
 
+template <int NT>
+static void launch_nt(dim3 grid, int M, int N, int K, const GemmA& a, const GemmB& b,
+                      const GemmEp& e, hipStream_t s) {
+    if (a.kind == 0)
+        hipLaunchKernelGGL((k_gemm<NT, 0>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    else if (a.kind == 1)
+        hipLaunchKernelGGL((k_gemm<NT, 1>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+    else
+        hipLaunchKernelGGL((k_gemm<NT, 2>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+}
+
 hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, const GemmEp& e,
                        hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    if (N >= 1024) {  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
-        dim3 grid((M + 63) / 64, (N + 255) / 256);
-        hipLaunchKernelGGL(k_gemm<4>, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
-    } else {
-        dim3 grid((M + 63) / 64, (N + 63) / 64);
-        hipLaunchKernelGGL(k_gemm<1>, grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
-    }
+    if (a.kind < 0 || a.kind > 2) return hipErrorInvalidValue;
+    if (N >= 1024)  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
+        launch_nt<4>(dim3((M + 63) / 64, (N + 255) / 256), M, N, K, a, b, e, s);
+    else
+        launch_nt<1>(dim3((M + 63) / 64, (N + 63) / 64), M, N, K, a, b, e, s);
     return hipGetLastError();
 }
 

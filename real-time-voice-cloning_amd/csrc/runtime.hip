@@ -1061,7 +1061,8 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         e4.Bu = Bu;
         e4.Btot = Btot;
         e4.row0 = row0;
-        HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
+        // the x4 P1 carries cI as its fourth column: the persistent kernels never read ws.cI
+        if (!(P1out && h->pw.p1x4)) HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
         if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
             const int np = h->pw.p1x4 ? 4 * H : 3 * H;  // (fatchord: + cI, unit-major)
             b4.p = h->pw.M1T;
@@ -1859,6 +1860,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                          g_err.c_str());
             h->persist_failed = true;
             use_p = false;
+            if (h->pw.p1x4)  // cI was not written (P1 carried it): conditioning again, cI only
+                for (int u = 0; u < n_utts; ++u)
+                    CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0,
+                                       S, Bp, plan[u].row0, plan[u].fbase, nullptr));
             h->last_B = Bp;  // chain runs every padded row (cI stride is Bp)
             rc = run_chain(h, S, cb, user);
             h->last_B = B;

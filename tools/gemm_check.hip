@@ -1,0 +1,161 @@
+// Standalone check of the precompute GEMM (kernels_gemm.hip) against a host f64 GEMM, for
+// the operand kinds the upsample / conditioning path uses. Build and run (GPU box):
+//   hipcc -O2 --offload-arch=gfx950 -I include -I real-time-voice-cloning_amd/csrc \
+//     tools/gemm_check.hip real-time-voice-cloning_amd/csrc/kernels_gemm.hip -o exp/gemm_check
+//   timeout -k 5 60 exp/gemm_check
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "wrnn_kernels.h"
+
+using namespace wrnn;
+
+#define HC(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(2);                                                             \
+        }                                                                             \
+    } while (0)
+
+static float* up(const std::vector<float>& v) {
+    float* d;
+    HC(hipMalloc(&d, v.size() * sizeof(float) + 256));
+    HC(hipMemcpy(d, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+    return d;
+}
+
+static std::vector<float> rnd(size_t n, unsigned s) {
+    std::vector<float> v(n);
+    for (auto& x : v) {
+        s = s * 1664525u + 1013904223u;
+        x = (float)((s >> 8) & 0xffff) / 65536.f - 0.5f;
+    }
+    return v;
+}
+
+// kind-0 A [M][K], kind-0 B [K][N], epilogue 0 (+bias[n]) or 3 (folded rows)
+static int case_plain(int M, int N, int K, int ep) {
+    auto A = rnd((size_t)M * K, 1 + M), B = rnd((size_t)K * N, 2 + N), bias = rnd(N, 3);
+    const int Bu = 3, Btot = 5, row0 = 1;
+    const int rows_out = ep == 3 ? ((M + Bu - 1) / Bu) * Btot : M;
+    float* dA = up(A);
+    float* dB = up(B);
+    float* db = up(bias);
+    float* dD;
+    HC(hipMalloc(&dD, (size_t)rows_out * N * sizeof(float)));
+    HC(hipMemset(dD, 0, (size_t)rows_out * N * sizeof(float)));
+    GemmA a{};
+    a.kind = 0;
+    a.p = dA;
+    a.ld = K;
+    GemmB b{};
+    b.kind = 0;
+    b.p = dB;
+    b.ld = N;
+    GemmEp e{};
+    e.kind = ep;
+    e.D = dD;
+    e.ld = N;
+    e.bias = db;
+    e.Bu = Bu;
+    e.Btot = Btot;
+    e.row0 = row0;
+    HC(launch_gemm(M, N, K, a, b, e, 0));
+    HC(hipDeviceSynchronize());
+    std::vector<float> D((size_t)rows_out * N);
+    HC(hipMemcpy(D.data(), dD, D.size() * sizeof(float), hipMemcpyDeviceToHost));
+    double worst = 0;
+    for (int m = 0; m < M; ++m) {
+        const size_t row = ep == 3 ? (size_t)(m / Bu) * Btot + row0 + m % Bu : (size_t)m;
+        for (int n = 0; n < N; ++n) {
+            double s = bias[n];
+            for (int k = 0; k < K; ++k) s += (double)A[(size_t)m * K + k] * B[(size_t)k * N + n];
+            worst = std::fmax(worst, std::fabs(s - D[row * N + n]));
+        }
+    }
+    std::printf("plain M=%d N=%d K=%d ep=%d: max |err| %.3g\n", M, N, K, ep, worst);
+    HC(hipFree(dA));
+    HC(hipFree(dB));
+    HC(hipFree(db));
+    HC(hipFree(dD));
+    return worst < 1e-3 ? 0 : 1;
+}
+
+// A gathers: kind 1 (conditioning rows from mel_up / R by fold position) and kind 2 (frames)
+static int case_gather(int kind, int M, int N) {
+    const int n_mel = 80, n_aux = 31, r_off = 32, C = 128, T = 40, hop = 20, Bu = 3, tpo = 30;
+    const int L = 700, ldm = 710, ldr = T;
+    const int K = kind == 1 ? n_mel + n_aux : 64;
+    auto mel = rnd((size_t)n_mel * ldm, 11), R = rnd((size_t)C * ldr, 12);
+    auto B = rnd((size_t)K * N, 13), bias = rnd(N, 14);
+    float *dmel = up(mel), *dR = up(R), *dB = up(B), *db = up(bias), *dD;
+    HC(hipMalloc(&dD, (size_t)M * N * sizeof(float)));
+    GemmA a{};
+    a.kind = kind;
+    a.mel = dmel;
+    a.ldm = ldm;
+    a.n_mel = n_mel;
+    a.L = L;
+    a.hop = hop;
+    a.R = dR;
+    a.ldr = ldr;
+    a.r_off = kind == 1 ? r_off : 7;
+    a.n_aux = n_aux;
+    a.Bu = Bu;
+    a.tpo = tpo;
+    GemmB b{};
+    b.kind = 0;
+    b.p = dB;
+    b.ld = N;
+    GemmEp e{};
+    e.kind = 0;
+    e.D = dD;
+    e.ld = N;
+    e.bias = db;
+    HC(launch_gemm(M, N, K, a, b, e, 0));
+    HC(hipDeviceSynchronize());
+    std::vector<float> D((size_t)M * N);
+    HC(hipMemcpy(D.data(), dD, D.size() * sizeof(float), hipMemcpyDeviceToHost));
+    double worst = 0;
+    for (int m = 0; m < M; ++m)
+        for (int n = 0; n < N; ++n) {
+            double s = bias[n];
+            for (int k = 0; k < K; ++k) {
+                double av = 0;
+                if (kind == 1) {
+                    const int p = (m % Bu) * tpo + m / Bu;
+                    if (p < L)
+                        av = k < n_mel ? mel[(size_t)k * ldm + p]
+                                       : R[(size_t)(r_off + k - n_mel) * ldr + p / hop];
+                } else if (m > 0) {
+                    av = R[(size_t)(a.r_off + k) * ldr + (m - 1)];
+                }
+                s += av * B[(size_t)k * N + n];
+            }
+            worst = std::fmax(worst, std::fabs(s - D[(size_t)m * N + n]));
+        }
+    std::printf("gather kind=%d M=%d N=%d K=%d: max |err| %.3g\n", kind, M, N, K, worst);
+    HC(hipFree(dmel));
+    HC(hipFree(dR));
+    HC(hipFree(dB));
+    HC(hipFree(db));
+    HC(hipFree(dD));
+    return worst < 1e-3 ? 0 : 1;
+}
+
+int main() {
+    int bad = 0;
+    bad += case_plain(70, 130, 37, 0);
+    bad += case_plain(200, 2048, 111, 3);
+    bad += case_plain(129, 1030, 16, 3);
+    bad += case_plain(64, 512, 128, 0);
+    bad += case_gather(1, 3 * 250, 512);
+    bad += case_gather(1, 3 * 250, 2048);
+    bad += case_gather(2, 41, 160);
+    std::printf(bad ? "FAIL\n" : "OK\n");
+    return bad;
+}
