@@ -166,6 +166,11 @@ int wrnn_stage_timing(wrnn_handle* h, int stage, double* avg_us, int* launches);
 int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, double* bytes,
                     double* flops, int* n_stages);
 
+/* Host post-processing helper (no device): de_emphasis of the reference,
+ * scipy.signal.lfilter([1], [1, -coef], x) (vocoder/audio.py:92-93, applied in
+ * fatchord_version.py:251-252), same doubles bit for bit. y may alias x. */
+int wrnn_de_emphasis(const double* x, double* y, size_t n, double coef);
+
 /* Raw access for tests: copy the RAW noise (seq_len, rows, n_classes) of the last call's
  * first `n_steps` steps to host (float32). */
 int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity);

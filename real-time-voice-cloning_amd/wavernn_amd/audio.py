@@ -45,6 +45,20 @@ def de_emphasis(x):
     return lfilter([1], [1, -sp.preemphasis], x)
 
 
+def de_emphasis_native(x, lib):
+    """de_emphasis through the library's host loop (wrnn_de_emphasis: scipy's lfilter
+    recurrence, same doubles), without scipy's generic filter machinery."""
+    import ctypes
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    pd = ctypes.POINTER(ctypes.c_double)
+    rc = lib.wrnn_de_emphasis(x.ctypes.data_as(pd), y.ctypes.data_as(pd), x.size,
+                              float(sp.preemphasis))
+    if rc:
+        raise RuntimeError('wrnn_de_emphasis failed (%d)' % rc)
+    return y
+
+
 def pre_emphasis(x):
     return lfilter([1, -sp.preemphasis], [1], x)
 
@@ -72,18 +86,42 @@ def xfade_and_unfold(y, target, overlap):
     return unfolded
 
 
+def _mu_law_unfolded(unfolded, labels, overlap, n_classes):
+    """decode_mu_law(unfolded, n_classes, False), element for element, for the output of
+    xfade_and_unfold over categorical rows: each fold's middle `target` samples are its labels'
+    values untouched (0 + v), so they are looked up in a table of the n_classes decoded label
+    values (the same numpy expression on the same f64 inputs); only the cross-faded overlaps
+    are decoded directly."""
+    num_folds, length = labels.shape
+    target = length - 2 * overlap
+    lut = decode_mu_law(labels_to_samples(np.arange(n_classes), n_classes).astype(np.float64),
+                        n_classes, False)
+    out = np.empty_like(unfolded)
+    out[:overlap] = decode_mu_law(unfolded[:overlap], n_classes, False)
+    # after the first overlap, fold i owns [middle (target) | overlap with fold i + 1]
+    u = unfolded[overlap:].reshape(num_folds, target + overlap)
+    o = out[overlap:].reshape(num_folds, target + overlap)
+    o[:, :target] = lut[labels[:, overlap:overlap + target].astype(np.intp)]
+    o[:, target:] = decode_mu_law(u[:, target:], n_classes, False)
+    return out
+
+
 def postprocess(samples, batched, target, overlap, mu_law, apply_preemphasis, n_classes,
-                wave_len, hop_length):
-    """fatchord_version.py:238-255 on the (B, S) per-fold samples (any float dtype)."""
+                wave_len, hop_length, labels=None, lib=None):
+    """fatchord_version.py:238-255 on the (B, S) per-fold samples (any float dtype).
+    ``labels``: the categorical rows the samples came from, if any (mu-law table path);
+    ``lib``: the loaded C-ABI library, if any (native de-emphasis loop)."""
     output = np.asarray(samples).astype(np.float64)
     if batched:
         output = xfade_and_unfold(output, target, overlap)
     else:
         output = output[0]
-    if mu_law:
+    if mu_law and batched and labels is not None and overlap > 0:
+        output = _mu_law_unfolded(output, np.asarray(labels), overlap, n_classes)
+    elif mu_law:
         output = decode_mu_law(output, n_classes, False)
     if apply_preemphasis:
-        output = de_emphasis(output)
+        output = de_emphasis_native(output, lib) if lib is not None else de_emphasis(output)
     fade_out = np.linspace(1, 0, 20 * hop_length)
     output = output[:wave_len]
     output[-20 * hop_length:] *= fade_out

@@ -310,7 +310,8 @@ class WaveRNN:
             smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
             wave_len = (int(m.shape[-1]) - 1) * self.hop_length
             wavs.append(postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
-                                    self.n_classes, wave_len, self.hop_length))
+                                    self.n_classes, wave_len, self.hop_length,
+                                    labels=rows if self.categorical else None, lib=self._lib))
         return wavs
 
     def generate(self, mels, batched, target, overlap, mu_law, apply_preemphasis,
@@ -326,7 +327,8 @@ class WaveRNN:
                                                    progress_callback)
         t1 = time.time()
         out = postprocess(samples, batched, target, overlap, mu_law, apply_preemphasis,
-                          self.n_classes, wave_len, self.hop_length)
+                          self.n_classes, wave_len, self.hop_length, labels=labels,
+                          lib=self._lib)
         self.timings = dict(device=t1 - t0, post=time.time() - t1, B=B, S=S)
         self.last_labels = labels
         self.last_samples = samples
