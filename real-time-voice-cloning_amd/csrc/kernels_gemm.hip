@@ -35,7 +35,10 @@ __device__ __forceinline__ ARow a_row(const GemmA& a, int m, int M) {
         r.s0 = r.s1 = 1;
         r.ksplit = 1 << 30;
     } else if constexpr (AK == 1) {  // cI: [mel_up(p) (n_mel) | aux(p // hop)[r_off : r_off + n_aux]]
-        const int p = (m % a.Bu) * a.tpo + m / a.Bu;  // fold_with_overlap position
+        // fold-major rows (m = fold * S + step, M = S * Bu): the 64 rows of a tile are
+        // consecutive positions of one or two folds, so each k reads whole cache lines
+        const int S = M / a.Bu, f = m / S, t = m - f * S;
+        const int p = f * a.tpo + t;  // fold_with_overlap position
         r.zero |= p >= a.L;                            // zero tail pad
         r.p0 = a.mel;
         r.o0 = p;
@@ -76,12 +79,7 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
         case 1:
             v = acc + e.bias[m];
             break;
-        case 3: {
-            const size_t row = (size_t)(m / e.Bu) * e.Btot + e.row0 + m % e.Bu;
-            e.D[row * e.ld + n] = acc + e.bias[n];
-            return;
-        }
-        default: {
+        default: {  // kind 2 (kind 3, the folded rows, is stored by k_gemm itself)
             // eval BatchNorm as torch CPU: x * (w / sqrt(var + eps)) + (b - mean * alpha)
             v = fmaf(acc, e.alpha[m], e.beta[m]);
             if (e.relu) v = v > 0.f ? v : 0.f;
@@ -102,7 +100,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
     __shared__ float Bs[16][64 * NT];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv & 1, wn = wv >> 1;
-    const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * NT;
+    // XCD-aware tile order: workgroup L runs on XCD L % 8; the column tiles of one row tile
+    // are consecutive workgroups of one XCD, so its L2 serves their shared A rows
+    const int n_tiles = (N + 64 * NT - 1) / (64 * NT), m_tiles = (M + 63) / 64;
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int m_tile = (local / n_tiles) * 8 + xcd, n_tile = local % n_tiles;
+    if (m_tile >= m_tiles) return;  // the row-tile count is padded to a multiple of 8
+    const int m0 = m_tile * 64, n0 = n_tile * 64 * NT;
     // this thread stages A(m0 + (tid & 63), k0 + (tid >> 6) + 4 i), i < 4
     const ARow ar = a_row<AK>(A, m0 + (tid & 63), M);
     float ra[4], rb[4 * NT];
@@ -145,6 +149,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
     }
     // C/D map (32x32, 16 regs): col = lane & 31, row = 8*(r>>2) + 4*(lane>>5) + (r&3)
     if (E.kind == 3) {  // folded rows: the row index once per r, the bias once per tile
+        const int S = M / E.Bu;  // fold-major m = fold * S + step, as the kind-1 A rows
         float bias[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -155,7 +160,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
         for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
             if (m >= M) continue;
-            float* D = E.D + ((size_t)(m / E.Bu) * E.Btot + E.row0 + m % E.Bu) * E.ld;
+            const int f = m / S, t = m - f * S;
+            float* D = E.D + ((size_t)t * E.Btot + E.row0 + f) * E.ld;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const int n = n0 + 64 * t + wn * 32 + (lane & 31);
@@ -190,10 +196,11 @@ hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, cons
                        hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (a.kind < 0 || a.kind > 2) return hipErrorInvalidValue;
+    const int m_tiles8 = ((M + 63) / 64 + 7) / 8 * 8;  // k_gemm's XCD-aware tile order
     if (N >= 1024)  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
-        launch_nt<4>(dim3((M + 63) / 64, (N + 255) / 256), M, N, K, a, b, e, s);
+        launch_nt<4>(dim3(m_tiles8 * ((N + 255) / 256)), M, N, K, a, b, e, s);
     else
-        launch_nt<1>(dim3((M + 63) / 64, (N + 63) / 64), M, N, K, a, b, e, s);
+        launch_nt<1>(dim3(m_tiles8 * ((N + 63) / 64)), M, N, K, a, b, e, s);
     return hipGetLastError();
 }
 

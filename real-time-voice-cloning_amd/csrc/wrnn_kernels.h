@@ -101,7 +101,7 @@ struct GemmA {  // A(m, k)
     int kind;   // 0: row-major W[m*ld + k]; 1: cond-A (mel/aux gather for cI); 2: frame-A
     const float* p;
     int ld;
-    // kind 1: row m = (step t = m / Bu, fold f = m % Bu) -> position p = f * tpo + t;
+    // kind 1: row m = (fold f = m / S, step t = m % S), S = M / Bu -> position p = f * tpo + t;
     // mel_up channel-major [n_mel][ldm] + R channel-major [C][T]
     const float* mel;
     int ldm, n_mel, L, hop;
@@ -117,7 +117,7 @@ struct GemmB {  // B(k, n)
 };
 struct GemmEp {
     int kind;   // 0: +bias[n]; 1: +bias[m]; 2: BN(m) [+relu] [+res];
-                // 3: +bias[n] into folded row (m / Bu) * Btot + row0 + m % Bu
+                // 3: +bias[n] into folded row t * Btot + row0 + f (m = f * S + t, S = M / Bu)
     int Bu, Btot, row0;
     float* D;
     int ld;

@@ -70,7 +70,9 @@ static int case_plain(int M, int N, int K, int ep) {
     HC(hipMemcpy(D.data(), dD, D.size() * sizeof(float), hipMemcpyDeviceToHost));
     double worst = 0;
     for (int m = 0; m < M; ++m) {
-        const size_t row = ep == 3 ? (size_t)(m / Bu) * Btot + row0 + m % Bu : (size_t)m;
+        // kind 3: fold-major m = fold * S + step -> folded row step * Btot + row0 + fold
+        const int S = M / Bu;
+        const size_t row = ep == 3 ? (size_t)(m % S) * Btot + row0 + m / S : (size_t)m;
         for (int n = 0; n < N; ++n) {
             double s = bias[n];
             for (int k = 0; k < K; ++k) s += (double)A[(size_t)m * K + k] * B[(size_t)k * N + n];
@@ -127,7 +129,8 @@ static int case_gather(int kind, int M, int N) {
             for (int k = 0; k < K; ++k) {
                 double av = 0;
                 if (kind == 1) {
-                    const int p = (m % Bu) * tpo + m / Bu;
+                    const int S = M / Bu;  // fold-major rows: m = fold * S + step
+                    const int p = (m / S) * tpo + m % S;
                     if (p < L)
                         av = k < n_mel ? mel[(size_t)k * ldm + p]
                                        : R[(size_t)(r_off + k - n_mel) * ldr + p / hop];
@@ -150,7 +153,7 @@ static int case_gather(int kind, int M, int N) {
 int main() {
     int bad = 0;
     bad += case_plain(70, 130, 37, 0);
-    bad += case_plain(200, 2048, 111, 3);
+    bad += case_plain(201, 2048, 111, 3);
     bad += case_plain(129, 1030, 16, 3);
     bad += case_plain(64, 512, 128, 0);
     bad += case_gather(1, 3 * 250, 512);
