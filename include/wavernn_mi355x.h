@@ -171,6 +171,23 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
  * fatchord_version.py:251-252), same doubles bit for bit. y may alias x. */
 int wrnn_de_emphasis(const double* x, double* y, size_t n, double coef);
 
+/* Host post-processing of categorical fold rows (no device), fatchord_version.py:238-255 with
+ * labels (nf, S) int16 from a batched RAW generate: xfade_and_unfold
+ * (fatchord_version.py:342-404), decode_mu_law (vocoder/audio.py), de_emphasis and the final
+ * fade, same doubles bit for bit as the reference's numpy / scipy path.
+ * wrnn_post_overlaps: the nf + 1 cross-faded overlap regions ((nf + 1) * overlap doubles), from
+ * samp[k] = the f64 value of label k (2k/(n-1) - 1 in fp32) and the fade_in / fade_out vectors
+ * of xfade_and_unfold; the caller decodes them (mu-law) itself.
+ * wrnn_post_assemble: the first n_out unfolded samples from mid_lut[k] (the value of a fold
+ * middle sample with label k) and the decoded regions, then de_emphasis (if preemph) and
+ * out[n_out - fade_len + i] *= fade[i]. Labels outside [0, n_classes) -> WRNN_ERR_INVALID. */
+int wrnn_post_overlaps(const int16_t* labels, int nf, int S, int overlap, const double* samp,
+                       int n_classes, const double* fade_in, const double* fade_out,
+                       double* regions);
+int wrnn_post_assemble(const int16_t* labels, int nf, int S, int overlap, const double* mid_lut,
+                       int n_classes, const double* regions, int preemph, double coef,
+                       const double* fade, size_t fade_len, double* out, size_t n_out);
+
 /* Raw access for tests: copy the RAW noise (seq_len, rows, n_classes) of the last call's
  * first `n_steps` steps to host (float32). */
 int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity);

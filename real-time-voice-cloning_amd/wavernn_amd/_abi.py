@@ -36,7 +36,7 @@ EXPORTED = [
     'wrnn_generate', 'wrnn_generate_batch_device', 'wrnn_enable_stage_timing',
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
-    'wrnn_de_emphasis',
+    'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble',
 ]
 
 
@@ -113,6 +113,11 @@ def load_library(path=None):
                                     P(ctypes.c_double), P(ctypes.c_double), P(c_int)]),
         'wrnn_de_emphasis': (c_int, [P(ctypes.c_double), P(ctypes.c_double), c_size_t,
                                      ctypes.c_double]),
+        'wrnn_post_overlaps': (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_void_p, c_void_p]),
+        'wrnn_post_assemble': (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_int, ctypes.c_double, c_void_p, c_size_t,
+                                       c_void_p, c_size_t]),
         'wrnn_debug_noise': (c_int, [c_void_p, c_int, P(ctypes.c_float), c_size_t]),
         'wrnn_debug_upsample': (c_int, [c_void_p, P(ctypes.c_float), c_size_t,
                                         P(ctypes.c_float), c_size_t]),

@@ -106,11 +106,75 @@ def _mu_law_unfolded(unfolded, labels, overlap, n_classes):
     return out
 
 
+_POST_TABLES = {}
+
+
+def _post_tables(n_classes, overlap, mu_law, fade_len):
+    """Per-(n_classes, overlap, mu_law, fade_len) tables of the fused label path: the f64 value
+    of every label, the middle-sample table (decoded if mu_law), xfade_and_unfold's fade_in /
+    fade_out and the final fade, each built with the reference's own numpy expressions."""
+    key = (n_classes, overlap, mu_law, fade_len)
+    t = _POST_TABLES.get(key)
+    if t is None:
+        samp = labels_to_samples(np.arange(n_classes), n_classes).astype(np.float64)
+        mid = decode_mu_law(samp, n_classes, False) if mu_law else samp.copy()
+        silence_len = overlap // 2
+        fade_len_x = overlap - silence_len
+        tt = np.linspace(-1, 1, fade_len_x, dtype=np.float64)
+        silence = np.zeros((silence_len), dtype=np.float64)
+        fade_in = np.ascontiguousarray(np.concatenate([silence, np.sqrt(0.5 * (1 + tt))]))
+        fade_out = np.ascontiguousarray(np.concatenate([np.sqrt(0.5 * (1 - tt)), silence]))
+        fade = np.ascontiguousarray(np.linspace(1, 0, fade_len))
+        t = _POST_TABLES[key] = (np.ascontiguousarray(samp), np.ascontiguousarray(mid),
+                                 fade_in, fade_out, fade)
+    return t
+
+
+def postprocess_labels(labels, target, overlap, mu_law, apply_preemphasis, n_classes,
+                       wave_len, hop_length, lib):
+    """postprocess() for batched categorical rows (labels (nf, S) int16), fused in the
+    library's host loops (wrnn_post_overlaps / wrnn_post_assemble): the same doubles as
+    xfade_and_unfold -> decode_mu_law -> de_emphasis -> fade, without the full-length
+    intermediates. Only the nf + 1 cross-faded overlap regions are decoded here, by the
+    reference's numpy expression; the middles come from a table of decoded label values.
+    Returns None when the shape is outside the fused path (the caller uses postprocess())."""
+    labels = np.ascontiguousarray(labels, dtype=np.int16)
+    nf, S = labels.shape
+    fade_len = 20 * hop_length
+    total = nf * (S - overlap) + overlap
+    n_out = min(int(wave_len), total)
+    if overlap < 1 or S < 2 * overlap + 1 or n_out < fade_len or wave_len < 0:
+        return None
+    samp, mid, fade_in, fade_out, fade = _post_tables(n_classes, overlap, bool(mu_law),
+                                                      fade_len)
+    regions = np.empty((nf + 1, overlap), np.float64)
+    rc = lib.wrnn_post_overlaps(labels.ctypes.data, nf, S, overlap, samp.ctypes.data,
+                                n_classes, fade_in.ctypes.data, fade_out.ctypes.data,
+                                regions.ctypes.data)
+    if rc:
+        raise RuntimeError('wrnn_post_overlaps failed (%d)' % rc)
+    if mu_law:
+        regions = np.ascontiguousarray(decode_mu_law(regions, n_classes, False))
+    out = np.empty(n_out, np.float64)
+    rc = lib.wrnn_post_assemble(labels.ctypes.data, nf, S, overlap, mid.ctypes.data,
+                                n_classes, regions.ctypes.data, int(bool(apply_preemphasis)),
+                                float(sp.preemphasis), fade.ctypes.data, fade_len,
+                                out.ctypes.data, n_out)
+    if rc:
+        raise RuntimeError('wrnn_post_assemble failed (%d)' % rc)
+    return out
+
+
 def postprocess(samples, batched, target, overlap, mu_law, apply_preemphasis, n_classes,
                 wave_len, hop_length, labels=None, lib=None):
     """fatchord_version.py:238-255 on the (B, S) per-fold samples (any float dtype).
     ``labels``: the categorical rows the samples came from, if any (mu-law table path);
     ``lib``: the loaded C-ABI library, if any (native de-emphasis loop)."""
+    if batched and labels is not None and lib is not None:
+        out = postprocess_labels(labels, target, overlap, mu_law, apply_preemphasis, n_classes,
+                                 wave_len, hop_length, lib)
+        if out is not None:
+            return out
     output = np.asarray(samples).astype(np.float64)
     if batched:
         output = xfade_and_unfold(output, target, overlap)

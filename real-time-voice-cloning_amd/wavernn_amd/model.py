@@ -19,7 +19,7 @@ import time
 import numpy as np
 
 from . import _abi
-from .audio import labels_to_samples, postprocess
+from .audio import labels_to_samples, postprocess, postprocess_labels
 
 MODEL_TYPE_FATCHORD = 'fatchord-wavernn'
 MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
@@ -307,8 +307,14 @@ class WaveRNN:
         wavs = []
         for u, m in enumerate(mels_dev):
             rows = host[roff[u]:roff[u + 1]]
-            smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
             wave_len = (int(m.shape[-1]) - 1) * self.hop_length
+            if self.categorical and batched:
+                wav = postprocess_labels(rows, target, overlap, mu_law, apply_preemphasis,
+                                         self.n_classes, wave_len, self.hop_length, self._lib)
+                if wav is not None:
+                    wavs.append(wav)
+                    continue
+            smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
             wavs.append(postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
                                     self.n_classes, wave_len, self.hop_length,
                                     labels=rows if self.categorical else None, lib=self._lib))

@@ -44,3 +44,39 @@ def test_native_de_emphasis_matches_lfilter(lib, size):
     got = audio.de_emphasis_native(x, lib)
     assert np.array_equal(got, ref)
     assert np.array_equal(np.signbit(got), np.signbit(ref))
+
+
+@pytest.mark.parametrize('mu_law,preemph', [(True, True), (False, True), (True, False),
+                                            (False, False)])
+@pytest.mark.parametrize('n,B,target,overlap,extra', [(512, 18, 11000, 550, -199),
+                                                      (1024, 5, 300, 51, 0),
+                                                      (512, 1, 1100, 550, 4000),
+                                                      (512, 4, 40, 1, -3)])
+def test_fused_label_post_bit_exact(lib, mu_law, preemph, n, B, target, overlap, extra):
+    """wrnn_post_overlaps / wrnn_post_assemble (one pass over the labels) against the plain
+    restatement: every mode flag, wave_len below and above the unfolded length."""
+    rng = np.random.default_rng(n * B + overlap)
+    lab = rng.integers(0, n, (B, target + 2 * overlap)).astype(np.int16)
+    lab[0, :3] = 0
+    lab[-1, -3:] = n - 1
+    smp = labels_to_samples(lab, n)
+    hop = 5
+    wave_len = B * (target + overlap) + overlap + extra
+    ref = audio.postprocess(smp, True, target, overlap, mu_law, preemph, n, wave_len, hop)
+    got = audio.postprocess_labels(lab, target, overlap, mu_law, preemph, n, wave_len, hop, lib)
+    assert got is not None and got.dtype == np.float64
+    assert np.array_equal(got, ref)
+    assert np.array_equal(np.signbit(got), np.signbit(ref))
+
+
+def test_fused_label_post_edges(lib):
+    lab = np.zeros((2, 30), np.int16)
+    # output shorter than the final fade: not the fused path (postprocess keeps the reference's
+    # own behaviour for it)
+    assert audio.postprocess_labels(lab, 10, 10, True, True, 512, 19, 1, lib) is None
+    lab[1, 4] = 512
+    with pytest.raises(RuntimeError):
+        audio.postprocess_labels(lab, 10, 10, True, True, 512, 50, 1, lib)
+    lab[1, 4] = -1
+    with pytest.raises(RuntimeError):
+        audio.postprocess_labels(lab, 10, 10, True, True, 512, 50, 1, lib)
