@@ -218,12 +218,21 @@ __global__ __launch_bounds__(kThreads) void k_mel_stencil(const float* in, int i
     const int W_out = W_in * s;
     const float* src = in + (size_t)c * T_in;
     float acc = 0.f;
-    for (int d = 0; d <= 2 * s; ++d) {
-        const int i = o + d - s;
-        if (i >= 0 && i < W_out) {
-            const int si = i / s - in_pad;
-            const float v = (si >= 0 && si < T_in) ? src[si] : 0.f;
-            acc = fmaf(w[d], v, acc);
+    // taps in d order (the same fma chain); the stretched index i / s is advanced
+    // incrementally instead of divided per tap (one division per output)
+    int d = 0, i = o - s;
+    if (i < 0) {
+        d = -i;
+        i = 0;
+    }
+    int q = i / s, r = i - q * s;
+    for (; d <= 2 * s && i < W_out; ++d, ++i) {
+        const int si = q - in_pad;
+        const float v = (si >= 0 && si < T_in) ? src[si] : 0.f;
+        acc = fmaf(w[d], v, acc);
+        if (++r == s) {
+            r = 0;
+            ++q;
         }
     }
     out[(size_t)c * ld_out + oo] = acc;
