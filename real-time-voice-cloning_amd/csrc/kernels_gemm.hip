@@ -93,11 +93,14 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
 // NT 64-wide column tiles per workgroup share one staged A tile (the gathered conditioning
 // rows are read once per k step, not once per column tile). The next k step's operands are
 // fetched into registers while the matrix cores work on the current one.
-template <int NT, int AK>
+// BK = k depth staged per step: 16 for the large conditioning GEMMs (K = 111), 64 for the small
+// launch-latency-bound MelResNet GEMMs (two to seven global round trips per tile instead of 8-25;
+// the k order of the MFMA chain is the same, so are the results).
+template <int NT, int AK, int BK>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
                                                    GemmEp E) {
-    __shared__ float As[16][64];
-    __shared__ float Bs[16][64 * NT];
+    __shared__ float As[BK][64];
+    __shared__ float Bs[BK][64 * NT];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wm = wv & 1, wn = wv >> 1;
     // XCD-aware tile order: workgroup L runs on XCD L % 8; the column tiles of one row tile
@@ -109,12 +112,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
     const int m0 = m_tile * 64, n0 = n_tile * 64 * NT;
     // this thread stages A(m0 + (tid & 63), k0 + (tid >> 6) + 4 i), i < 4
     const ARow ar = a_row<AK>(A, m0 + (tid & 63), M);
-    float ra[4], rb[4 * NT];
+    float ra[BK / 4], rb[BK / 4 * NT];
     auto fetch = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[i] = load_a(ar, k0 + (tid >> 6) + 4 * i, K);
+        for (int i = 0; i < BK / 4; ++i) ra[i] = load_a(ar, k0 + (tid >> 6) + 4 * i, K);
 #pragma unroll
-        for (int i = 0; i < 4 * NT; ++i) {
+        for (int i = 0; i < BK / 4 * NT; ++i) {
             const int e = tid + i * kThreads;
             const int n = n0 + e % (64 * NT), k = k0 + e / (64 * NT);
             rb[i] = (n < N && k < K) ? load_b(B, k, n) : 0.f;
@@ -126,18 +129,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
     fetch(0);
-    for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int k0 = 0; k0 < K; k0 += BK) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) As[(tid >> 6) + 4 * i][tid & 63] = ra[i];
+        for (int i = 0; i < BK / 4; ++i) As[(tid >> 6) + 4 * i][tid & 63] = ra[i];
 #pragma unroll
-        for (int i = 0; i < 4 * NT; ++i) {
+        for (int i = 0; i < BK / 4 * NT; ++i) {
             const int e = tid + i * kThreads;
             Bs[e / (64 * NT)][e % (64 * NT)] = rb[i];
         }
         __syncthreads();
-        if (k0 + 16 < K) fetch(k0 + 16);
+        if (k0 + BK < K) fetch(k0 + BK);
 #pragma unroll
-        for (int kp = 0; kp < 8; ++kp) {
+        for (int kp = 0; kp < BK / 2; ++kp) {
             const float av = As[2 * kp + (lane >> 5)][wm * 32 + (lane & 31)];
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -181,15 +184,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
         }
 }
 
-template <int NT>
+template <int NT, int BK>
 static void launch_nt(dim3 grid, int M, int N, int K, const GemmA& a, const GemmB& b,
                       const GemmEp& e, hipStream_t s) {
     if (a.kind == 0)
-        hipLaunchKernelGGL((k_gemm<NT, 0>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+        hipLaunchKernelGGL((k_gemm<NT, 0, BK>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
     else if (a.kind == 1)
-        hipLaunchKernelGGL((k_gemm<NT, 1>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+        hipLaunchKernelGGL((k_gemm<NT, 1, BK>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
     else
-        hipLaunchKernelGGL((k_gemm<NT, 2>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
+        hipLaunchKernelGGL((k_gemm<NT, 2, BK>), grid, dim3(kThreads), 0, s, M, N, K, a, b, e);
 }
 
 hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, const GemmEp& e,
@@ -198,9 +201,13 @@ hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, cons
     if (a.kind < 0 || a.kind > 2) return hipErrorInvalidValue;
     const int m_tiles8 = ((M + 63) / 64 + 7) / 8 * 8;  // k_gemm's XCD-aware tile order
     if (N >= 1024)  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
-        launch_nt<4>(dim3(m_tiles8 * ((N + 255) / 256)), M, N, K, a, b, e, s);
+        launch_nt<4, 16>(dim3(m_tiles8 * ((N + 255) / 256)), M, N, K, a, b, e, s);
+    else if ((M + 63) / 64 * ((N + 63) / 64) <= 256 && K >= 64)
+        // fewer tiles than CUs (MelResNet: M = 128 channels, N = frames): latency-bound, so
+        // stage k 64 deep (one global round trip per 64 k instead of per 16)
+        launch_nt<1, 64>(dim3(m_tiles8 * ((N + 63) / 64)), M, N, K, a, b, e, s);
     else
-        launch_nt<1>(dim3(m_tiles8 * ((N + 63) / 64)), M, N, K, a, b, e, s);
+        launch_nt<1, 16>(dim3(m_tiles8 * ((N + 63) / 64)), M, N, K, a, b, e, s);
     return hipGetLastError();
 }
 

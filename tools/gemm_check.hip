@@ -156,6 +156,8 @@ int main() {
     bad += case_plain(201, 2048, 111, 3);
     bad += case_plain(129, 1030, 16, 3);
     bad += case_plain(64, 512, 128, 0);
+    bad += case_plain(128, 996, 400, 0);  // 64-deep k staging, K padded (MelResNet conv_in)
+    bad += case_plain(130, 70, 77, 0);
     bad += case_gather(1, 3 * 250, 512);
     bad += case_gather(1, 3 * 250, 2048);
     bad += case_gather(2, 41, 160);
