@@ -55,6 +55,24 @@ def test_postprocess_matches_reference_waveform(name):
     assert np.array_equal(wav, gold['wav'])
 
 
+@pytest.mark.parametrize('name', ['fatchord_raw9_tiny', 'fatchord_raw9_config1',
+                                  'fatchord_raw10_defaults', 'runtimeracer_raw9_tiny'])
+def test_fused_label_post_matches_reference_waveform(name):
+    """The library's fused label post-processing (wrnn_post_overlaps / wrnn_post_assemble)
+    reproduces the reference waveform of each batched RAW fixture bit for bit."""
+    from wavernn_amd import _abi
+    from wavernn_amd.audio import postprocess_labels
+    meta, gold = golden_case(name)
+    if not meta['batched'] or meta['mode'] != 'RAW':
+        pytest.skip('fused path covers batched categorical rows')
+    hp = hparams_of(meta)
+    wav = postprocess_labels(gold['labels'], meta['target'], meta['overlap'], hp.mu_law, True,
+                             2 ** meta['bits'], (meta['n_frames'] - 1) * 200, 200,
+                             _abi.load_library())
+    assert wav is not None
+    assert np.array_equal(wav, gold['wav'])
+
+
 def test_short_mel_raises_like_reference():
     """wave_len < 20*hop: the reference's fade-out broadcast fails (fatchord_version.py:255)."""
     from wavernn_amd.audio import postprocess
