@@ -193,6 +193,21 @@ def main():
         'cpu_baseline': None,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        # PCIe-inclusive rate of the drop-in host-buffer API (WaveRNN.generate as
+        # infer_waveform calls it: host mel in, f64 waveform out, progress callback every 100
+        # steps, so the persistent engine runs in launches of 1000 steps). Reported, never
+        # `value` (whose inputs are resident in HBM).
+        mel0 = (mels_host[0] / sp.max_abs_value).astype(np.float32)
+        model.generate(mel0, True, args.target, args.overlap, hp.mu_law, sp.preemphasize,
+                       progress_callback=lambda *a: None)
+        th = time.perf_counter()
+        wav = model.generate(mel0, True, args.target, args.overlap, hp.mu_law,
+                             sp.preemphasize, progress_callback=lambda *a: None)
+        th = time.perf_counter() - th
+        result['dropin_host_io'] = {
+            'value': len(wav) / th, 'unit': 'samples/s', 'ms': th * 1e3,
+            'path': 'WaveRNN.generate(host mel) -> f64 waveform: H2D mel, labels D2H, '
+                    'progress callback every 100 steps (persist launches of 1000 steps)'}
         result['cpu_baseline'] = cpu_baseline(args, sd, hp, mels_host[0])
     if rank == 0:
         print(json.dumps(result), flush=True)
