@@ -8,11 +8,14 @@ step   : one generate() over the per-GPU batch: upsample + conditioning + the fu
 N=1    : BASELINE configs[1]: one 1000-frame mel, fatchord 9-bit mu-law RAW, target=11000,
          overlap=550 (18 folds x 12,100 steps).
 N>1    : one process per GPU (torchrun); utterances are independent, so each rank runs its own
-         (weak scaling, no data-path collective); --utts-per-gpu 8 --gpus 8 is configs[3]
-         (64 utterances on 8 GPUs).
-Also reported: roofline of the dominant recurrent kernel (in-kernel s_memrealtime stamps over
-the timed region) and the CPU baseline (oracle restatement of the reference generate(), timed
-on this host on a bounded sample of the same workload, rank 0, N=1 only).
+         shard (weak scaling, no collective on the data path); the fold rows are gathered to
+         rank 0 (one RCCL gather) which post-processes every utterance (wavernn_amd.distributed).
+         --utts-per-gpu 8 --gpus 8 is configs[3] (64 utterances on 8 GPUs).
+Also reported: roofline of the dominant recurrent kernel (HIP events on its stream over the
+timed region; HBM, fp32 and latency-floor fractions), the CPU baseline (oracle restatement of
+the reference generate() on this host: the whole utterance on the default thread count, plus
+bounded 1-thread and all-core legs; rank 0, N=1 only) and `parity`: the timed call's labels and
+waveform against that same oracle run (same seed and noise stream).
 """
 import argparse
 import json
@@ -67,27 +70,96 @@ def _cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(args, sd, hp, mel):
-    """Oracle (torch-CPU restatement of the reference generate) on a bounded sample."""
+# Latency model of the persistent recurrence: per step, `hops` in-group
+# exchanges at the guide's one-to-one hand-off latency (MI355X_MICROARCH.md price list,
+# handoff-1to1: 0.8 us idle for an 8-byte granule) plus the critical-path products of one
+# workgroup at the fp32 vector peak (64 FLOP/clk/SIMD x 4 SIMDs x 2.4 GHz).
+HANDOFF_US = 0.8
+CU_FP32_FLOP_PER_US = 64 * 4 * 2400.0
+PERSIST_HOPS = {'fatchord-wavernn': 4, 'runtimeracer-wavernn': 8, 'geneing-wavernn': 2}
+
+
+def latency_floor_us(model_type, hp, rows_per_group, n_classes):
+    """Lower bound of one persistent step: exchange hops + critical products of one slot."""
+    H, F = hp.rnn_dims, hp.fc_dims
+    slots = 32
+    if model_type == 'fatchord-wavernn':      # GRU2 (3H x H) -> fc1 -> fc2 -> fc3
+        crit = 3 * H * H + F * H + F * F + n_classes * F
+    elif model_type == 'runtimeracer-wavernn':  # GRU2, GRU3, GRU4, fc1..fc5
+        crit = 3 * (3 * H * H) + F * H + F * F + F * F + F * F + n_classes * F
+    else:                                       # geneing: fc1 -> fc3
+        crit = F * H + n_classes * F
+    flop = 2.0 * crit * rows_per_group / slots
+    hops = PERSIST_HOPS[model_type]
+    return hops * HANDOFF_US + flop / CU_FP32_FLOP_PER_US, hops
+
+
+def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0):
     import torch
     from oracle.wavernn_oracle import OracleWaveRNN
-    cores = torch.get_num_threads()
+    torch.set_num_threads(threads)
     o = OracleWaveRNN(sd, hp, args.model)
     m = torch.from_numpy(mel[None] / 4.0)
-    # calibrate: time 50 steps, then size the sample to ~cpu_seconds
-    probe = o.generate(m, True, args.target, args.overlap, hp.mu_law, True, max_steps=50)
-    per_step = probe['t_loop'] / 50
-    k = int(max(100, min(probe['S'], args.cpu_seconds / max(per_step, 1e-6))))
-    r = o.generate(m, True, args.target, args.overlap, hp.mu_law, True, max_steps=k)
-    S = r['S']
-    t_total = r['t_prepare'] + r['t_loop'] * S / r['steps']
+    t0 = time.perf_counter()
+    r = o.generate(m, True, args.target, args.overlap, hp.mu_law, True, max_steps=max_steps,
+                   seed=seed, stream=stream)
+    r['t_wall'] = time.perf_counter() - t0
+    return r
+
+
+def _bounded_leg(args, sd, hp, mel, threads, seconds):
+    """Oracle on `threads` host threads: upsample + the first k steps (k sized to ~seconds),
+    the loop time extrapolated to all S steps."""
+    probe = _oracle_run(args, sd, hp, mel, threads, max_steps=20)
+    per_step = probe['t_loop'] / 20
+    k = int(max(50, min(probe['S'], seconds / max(per_step, 1e-6))))
+    r = _oracle_run(args, sd, hp, mel, threads, max_steps=k)
+    t_total = r['t_prepare'] + r['t_loop'] * r['S'] / r['steps']
     samples = (args.frames - 1) * 200
-    return dict(value=samples / t_total, unit='samples/s', cores=cores, kind='port',
-                cpu_model=_cpu_model(), affinity_cpus=len(os.sched_getaffinity(0)),
-                sample=f"oracle.wavernn_oracle (torch-CPU restatement of reference generate()), "
-                       f"{args.model} {args.mode} {args.bits}-bit, T={args.frames}: upsample + first "
-                       f"{r['steps']} of {S} steps ({r['B']} folds), loop time extrapolated to all "
-                       f"steps; {r['t_prepare'] + r['t_loop']:.1f}s measured")
+    return dict(value=samples / t_total, unit='samples/s', cores=threads,
+                sample=f"upsample + first {r['steps']} of {r['S']} steps ({r['B']} folds), loop "
+                       f"extrapolated to all steps; {r['t_prepare'] + r['t_loop']:.1f}s measured")
+
+
+def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
+    """The oracle (torch-CPU restatement of the reference generate(), pinned bit-exact to the
+    reference by tests/test_oracle_golden.py) on this host's cores.
+
+    Leg 1 (`value`): the WHOLE workload of utterance 0 (all S steps, upsample, post) with
+    torch's default thread count (OMP_NUM_THREADS: the box's CPU share), on the GPU run's own
+    (seed, stream), so its labels / waveform are also the parity check of the timed GPU call.
+    Legs 2 / 3: bounded samples with 1 thread and with every core in the affinity mask
+    (all host cores and one core)."""
+    import numpy as np
+    import torch
+    threads = torch.get_num_threads()
+    n_aff = len(os.sched_getaffinity(0))
+    r = _oracle_run(args, sd, hp, mel, threads, seed=seed, stream=stream)
+    samples = (args.frames - 1) * 200
+    parity = {'rows': int(r['B']), 'steps': int(r['S']), 'seed': seed, 'stream': stream}
+    if r['labels'] is not None:
+        diff = np.argwhere(gpu_rows != r['labels'])
+        parity['labels_equal'] = bool(len(diff) == 0)
+        parity['label_agreement'] = float((gpu_rows == r['labels']).mean())
+        parity['first_divergence'] = (None if len(diff) == 0 else
+                                      [int(v) for v in diff[np.argmin(diff[:, 1])]])
+        parity['wave_bit_exact'] = bool(np.array_equal(gpu_wav, r['wav']))
+    else:
+        parity['samples_rms'] = float(np.sqrt(np.mean((gpu_rows.astype(np.float64) -
+                                                        r['samples']) ** 2)))
+        parity['wave_rms'] = float(np.sqrt(np.mean((gpu_wav - r['wav']) ** 2)))
+        parity['tolerance'] = 1e-4
+    legs = [dict(value=samples / r['t_wall'], unit='samples/s', cores=threads,
+                 sample=f"whole utterance: {r['B']} folds x {r['S']} steps + upsample + post, "
+                        f"{r['t_wall']:.1f}s")]
+    legs.append(_bounded_leg(args, sd, hp, mel, 1, args.cpu_seconds / 2))
+    if n_aff > 1 and n_aff != threads:
+        legs.append(_bounded_leg(args, sd, hp, mel, n_aff, args.cpu_seconds / 3))
+    torch.set_num_threads(threads)
+    out = dict(legs[0], kind='port', cpu_model=_cpu_model(), affinity_cpus=n_aff, legs=legs)
+    out['sample'] = (f"oracle.wavernn_oracle (torch-CPU restatement of reference generate()), "
+                     f"{args.model} {args.mode} {args.bits}-bit, T={args.frames}, " + legs[0]['sample'])
+    return out, parity
 
 
 def main():
@@ -97,6 +169,7 @@ def main():
     import torch.distributed as dist
     from wavernn_amd.model import WaveRNN
     from wavernn_amd.base import hparams_for
+    from wavernn_amd.distributed import infer_waveforms, shard
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_state_dict, synth_mel
 
@@ -115,17 +188,34 @@ def main():
                     hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
                     mode=hp.mode, model_type=args.model, device=local)
     model.load_state_dict(sd)
-    model.set_seed(1234)
+    seed = 1234
+    model.set_seed(seed)
     model.set_engine(args.engine)
     U = args.utts_per_gpu
-    mels_host = [synth_mel(args.frames, seed=rank * U + u) for u in range(U)]
-    mels_dev = [torch.from_numpy(m / sp.max_abs_value).to(dev) for m in mels_host]
+    n_utts = U * world
+    # every rank knows every utterance's length; only its own shard is resident in its HBM
+    mels_host = [synth_mel(args.frames, seed=i) for i in range(n_utts)]
+    plan = shard([args.frames] * n_utts, world, args.target, args.overlap)
+    mine = set(plan[rank])
+    mels = [torch.from_numpy((m / sp.max_abs_value).astype(np.float32)).to(dev) if i in mine
+            else m for i, m in enumerate(mels_host)]
+    S = model.fold_shape(args.frames, True, args.target, args.overlap)[1]
     if not args.no_timing:
         model.enable_stage_timing(True)
+    last = {}
+
+    def rows_fn(ms):
+        out, roff, _ = model.generate_batch_device(ms, True, args.target, args.overlap)
+        last['rows'], last['roff'] = out, roff
+        return out, roff
+
+    def post_fn(rows, n_frames):
+        return model.postprocess_rows(rows, n_frames, True, args.target, args.overlap, hp.mu_law,
+                                      sp.preemphasize)
 
     def step():
-        return model.generate_batch(mels_dev, True, args.target, args.overlap, hp.mu_law,
-                                    sp.preemphasize)
+        # the whole job: fold recurrence per rank, labels gathered to rank 0 (RCCL), f64 post
+        return infer_waveforms(mels, rows_fn, post_fn, args.target, args.overlap, S, device=dev)
 
     for _ in range(args.warmup):
         wavs = step()
@@ -143,14 +233,18 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    samples_per_step = sum(len(w) for w in wavs)
-    total_samples = samples_per_step * args.steps * world
+    samples_per_step = n_utts * (args.frames - 1) * sp.hop_size
+    if rank == 0:
+        assert wavs is not None and sum(len(w) for w in wavs) == samples_per_step
+    total_samples = samples_per_step * args.steps
     value = total_samples / dt
 
-    workload = (f'{U}x{args.frames}-frame mel per GPU, {args.model} {args.mode} {args.bits}-bit mu-law, '
+    wname = 'MOL' if mode == 'MOL' else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else '')
+    workload = (f'{U}x{args.frames}-frame mel per GPU, {args.model} {wname}, '
                 f'batched folds target={args.target} overlap={args.overlap}')
     roof = None
     info = model.stage_info() if not args.no_timing else []
+    rows_per_gpu = U * model.fold_shape(args.frames, True, args.target, args.overlap)[0]
     if info:
         # dominant kernel = largest avg duration x launches
         dom = max(info, key=lambda r: (r[3] if r[3] == r[3] else 0) * r[4])
@@ -163,11 +257,18 @@ def main():
                 'avg_us': us, 'launches_timed': n, 'alg_bytes_per_launch': by,
                 'flops_per_launch': fl,
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
+                'fp32_frac': fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
-        if name == 'persist':  # no progress callback -> one launch per row batch runs all S steps
-            S = model.fold_shape(args.frames, True, args.target, args.overlap)[1]
+        if name == 'persist':  # one launch per row batch runs all S steps
             roof['us_per_step'] = us / S
             roof['launches_per_generate'] = n  # stage timing keeps the last generate's launches
+            nr = -(-rows_per_gpu // (8 * n)) if n else 0
+            floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes)
+            roof['latency_floor_us'] = floor
+            roof['latency_frac'] = floor / roof['us_per_step']
+            roof['latency_model'] = (f'{hops} in-group hops x {HANDOFF_US} us (handoff-1to1) + '
+                                     f'critical products of one slot at the fp32 vector peak, '
+                                     f'{nr} rows per XCD group')
         # HBM traffic of the same kernel on the same workload from the committed PMC passes
         # (rocprofv3 cannot run inside this process; profiles/pmc_traffic.json names its source)
         pmc = _pmc_traffic(kernel, workload)
@@ -175,6 +276,7 @@ def main():
             roof['traffic'] = pmc['traffic_bytes']
             roof['traffic_source'] = pmc['source']
             roof['traffic_note'] = pmc['correction']
+    fb = model.fallback_info()
     result = {
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',
         'value': value, 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -185,18 +287,24 @@ def main():
         'xrtf': value / sp.sample_rate,
         'config': {'workload': workload,
                    'utts_per_gpu': U, 'frames': args.frames,
-                   'fold_rows_per_gpu': U * model.fold_shape(args.frames, True, args.target,
-                                                             args.overlap)[0],
-                   'parallelism': f'utterances sharded over {world} GPU(s), no collective',
-                   'engine': model.last_engine()},
+                   'fold_rows_per_gpu': rows_per_gpu,
+                   'parallelism': (f'utterances sharded over {world} GPU(s); fold rows gathered '
+                                   f'to rank 0 (RCCL gather), f64 post-processing on rank 0'
+                                   if world > 1 else 'one GPU'),
+                   'engine': model.last_engine(), 'persist_fallbacks': fb[0]},
         'roofline': roof,
         'cpu_baseline': None,
     }
+    if fb[0]:
+        result['config']['fallback_reason'] = fb[1]
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        # parity of the last timed call: utterance 0's fold rows and waveform against the oracle
+        gpu_rows = last['rows'].cpu().numpy()[last['roff'][0]:last['roff'][1]]
+        stream = (args.warmup + args.steps - 1) * U
         # PCIe-inclusive rate of the drop-in host-buffer API (WaveRNN.generate as
-        # infer_waveform calls it: host mel in, f64 waveform out, progress callback every 100
-        # steps, so the persistent engine runs in launches of 1000 steps). Reported, never
-        # `value` (whose inputs are resident in HBM).
+        # infer_waveform calls it: host mel in, f64 waveform out, the reference's progress
+        # callback at i % 100 == 0 -- one persistent launch, progress read from host-mapped
+        # memory). Reported, never `value` (whose inputs are resident in HBM).
         mel0 = (mels_host[0] / sp.max_abs_value).astype(np.float32)
         model.generate(mel0, True, args.target, args.overlap, hp.mu_law, sp.preemphasize,
                        progress_callback=lambda *a: None)
@@ -207,8 +315,9 @@ def main():
         result['dropin_host_io'] = {
             'value': len(wav) / th, 'unit': 'samples/s', 'ms': th * 1e3,
             'path': 'WaveRNN.generate(host mel) -> f64 waveform: H2D mel, labels D2H, '
-                    'progress callback every 100 steps (persist launches of 1000 steps)'}
-        result['cpu_baseline'] = cpu_baseline(args, sd, hp, mels_host[0])
+                    'progress callback at i % 100 == 0 (reference cadence)'}
+        result['cpu_baseline'], result['parity'] = cpu_baseline(args, sd, hp, mels_host[0],
+                                                                gpu_rows, wavs[0], seed, stream)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

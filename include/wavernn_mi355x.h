@@ -84,9 +84,12 @@ typedef struct wrnn_config {
 
 typedef struct wrnn_handle wrnn_handle;
 
-/* Called every 100 steps with the reference's progress_callback arguments
- * (fatchord_version.py:234-236): step index i, seq_len, b_size, gen_rate in kHz.
- * Return non-zero to abort generation (WRNN_ERR_ABORTED). */
+/* Called at i = 0, 100, 200, ... < seq_len, in order, once each, with the reference's
+ * progress_callback arguments (fatchord_version.py:234-236): step index i, seq_len, b_size,
+ * gen_rate in kHz -- as soon as every fold row has finished step i (PERSIST: the kernels
+ * publish their step count to host-mapped memory; CHAIN: between 100-step graphs). Return
+ * non-zero to abort (WRNN_ERR_ABORTED): no further callbacks; PERSIST stops at the end of the
+ * running launch. */
 typedef int (*wrnn_progress_fn)(void* user, int i, int seq_len, int b_size, double gen_rate_khz);
 
 /* Library / device info. */
@@ -155,6 +158,12 @@ int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* m
 int wrnn_set_engine(wrnn_handle* h, int engine);
 /* Engine that ran the last call. */
 int wrnn_last_engine(wrnn_handle* h, int* engine);
+/* Calls on this handle that fell back from PERSIST to CHAIN under WRNN_ENGINE_AUTO (the
+ * persistent launch could not run, e.g. its 256 workgroups did not become co-resident), and
+ * the last reason (NUL-terminated, truncated to reason_cap). Each fallback also prints a
+ * warning to stderr; with WRNN_ENGINE_PERSIST requested the call fails instead. AUTO stops
+ * trying PERSIST after 3 failed calls in a row. */
+int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_cap);
 
 /* Per-stage timing of the dominant recurrent kernel. Enable before a call; read after:
  * average duration in microseconds of the launches of stage `stage` in the last call, and

@@ -72,29 +72,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const int tid = threadIdx.x;
     // ---- group formation (placement-independent: a group is whatever shares an XCD) ----
     if (tid == 0) {
-        unsigned x;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-        const int g = x & 7;
-        s_group = g;
-        s_slot = (int)atomicAdd(a.ctl + PC_REG + g, 1u);
-        atomicAdd(a.ctl + PC_TOTAL, 1u);
-        const unsigned t0 = p_now();
-        int ok = 1;
-        while (ld_sc1_u(a.ctl + PC_TOTAL) < (unsigned)(kPG * kPM)) {
-            __builtin_amdgcn_s_sleep(1);
-            if (p_now() - t0 > kSpinTicks) {
-                ok = 0;
-                atomicMax(a.ctl + PC_ERR, 1u);
-                break;
-            }
-        }
-        if (ok)
-            for (int i = 0; i < kPG; ++i)
-                if (ld_sc1_u(a.ctl + PC_REG + i) != (unsigned)kPM) {
-                    ok = 0;
-                    atomicMax(a.ctl + PC_ERR, 3u);
-                }
-        s_ok = ok;
+        int gg, ss;
+        s_ok = p_register(a.ctl, gg, ss);
+        s_group = gg;
+        s_slot = ss;
     }
     __syncthreads();
     if (!s_ok) return;
@@ -665,6 +646,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X1 + r * kPH + tid] = hn;
         }
         pgum = pgn;
+        if (g == 0 && w == 0 && tid == 0) p_progress(a.progress, a.prog_base, t);
         __syncthreads();
         PSTAMP(10);
     }

@@ -71,6 +71,44 @@ __device__ __forceinline__ void dot4(v2f& acc, const float4 w, const float4 x) {
 }
 __device__ __forceinline__ float hsum(const v2f a) { return a.x + a.y; }
 
+// Group formation of the persistent kernels, run by thread 0 of every workgroup: a group is
+// whatever shares an XCD (HW_REG_XCC_ID), placement-independent. Returns 1 when all kPG * kPM
+// workgroups registered, 32 per XCD; 0 (with PC_ERR set) on a registration timeout, a bad
+// spread, or an error an earlier launch of the same call left in PC_ERR -- so a call whose
+// first launch could not become co-resident drains its queued launches at once.
+__device__ __forceinline__ int p_register(unsigned* ctl, int& group, int& slot) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    group = (int)(x & 7);
+    slot = (int)atomicAdd(ctl + PC_REG + group, 1u);
+    atomicAdd(ctl + PC_TOTAL, 1u);
+    const unsigned t0 = p_now();
+    while (ld_sc1_u(ctl + PC_TOTAL) < (unsigned)(kPG * kPM)) {
+        if (ld_sc1_u(ctl + PC_ERR)) return 0;
+        __builtin_amdgcn_s_sleep(1);
+        if (p_now() - t0 > kSpinTicks) {
+            atomicMax(ctl + PC_ERR, 1u);
+            return 0;
+        }
+    }
+    if (ld_sc1_u(ctl + PC_ERR)) return 0;
+    for (int i = 0; i < kPG; ++i)
+        if (ld_sc1_u(ctl + PC_REG + i) != (unsigned)kPM) {
+            atomicMax(ctl + PC_ERR, 3u);
+            return 0;
+        }
+    return 1;
+}
+
+// Progress of a launch for the host's progress callback (fatchord_version.py:234-236 calls
+// back at i % 100 == 0): after step t with t % 100 == 0, one lane publishes base + t + 1
+// steps done to a host-mapped word (vector store, system scope); the host polls it while the
+// launch runs. base = row batch * S.
+__device__ __forceinline__ void p_progress(unsigned* prog, int base, int t) {
+    if (prog != nullptr && t % kProgressEvery == 0)
+        __hip_atomic_store(prog, (unsigned)(base + t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
     const int rel = ri.rel0 + t;
     return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;

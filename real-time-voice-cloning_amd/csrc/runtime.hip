@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -191,7 +192,12 @@ struct wrnn_handle {
     } pws;
     int engine = WRNN_ENGINE_AUTO;  // requested engine (wrnn_set_engine / env WRNN_ENGINE)
     int last_engine = WRNN_ENGINE_CHAIN;
-    bool persist_failed = false;    // a persistent launch failed on this device: stay on CHAIN
+    bool persist_failed = false;    // kPersistMaxStreak persistent calls in a row failed: CHAIN
+    int persist_fail_streak = 0;    // consecutive persistent calls that fell back
+    int fallbacks = 0;              // calls on this handle that fell back PERSIST -> CHAIN
+    std::string fallback_reason;    // why the last one did
+    unsigned* prog_host = nullptr;  // host-mapped progress word (kernels publish steps done)
+    unsigned* prog_dev = nullptr;
     int last_Bp = 0;                // rows the last call ran (padded to 8 * rows-per-group)
     int p_nr = 0, p_nbatch = 0;     // PERSIST: rows per group per launch, row batches
     std::vector<hipEvent_t> pev;    // PERSIST timing events (start, end) per launch
@@ -204,6 +210,7 @@ struct wrnn_handle {
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         if (rows_ready) (void)hipEventDestroy(rows_ready);
         if (noise_done) (void)hipEventDestroy(noise_done);
+        if (prog_host) (void)hipHostFree(prog_host);
         if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1388,6 +1395,7 @@ int run_chain(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
 
 constexpr double kPersistWsBytes = 96.0 * (1 << 30);  // P1 + cI + noise cap (of 288 GB HBM)
 constexpr int kPersistFallback = 1;  // internal: retry the call on the CHAIN engine
+constexpr int kPersistMaxStreak = 3; // consecutive failed persistent calls before AUTO stops trying
 
 bool persist_device_ok(wrnn_handle* h) {
     static int cached[64];  // 0 unknown, 1 ok, 2 not ok (per device ordinal)
@@ -1609,49 +1617,41 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(launch_persist_init(a, st));
     }
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
-    // launches: row batches in order, each in time chunks (1000 steps when a progress callback
-    // wants reports, else one chunk); the step tags restart with every batch, so the exchange
-    // area and flags are cleared before each batch's first chunk
+    // launches: one per row batch, each running all S steps; the step tags restart with every
+    // batch, so the exchange area and flags are cleared before each. A progress callback does
+    // not split launches: the kernels publish their step count to a host-mapped word every 100
+    // steps (persist_common.h p_progress) and this thread reports from it while they run.
     const int nb = h->p_nbatch;
     a.nr = h->p_nr;
-    const int G = cb ? 1000 : S;
-    const int nchunks = (S + G - 1) / G;
-    const int nl = nb * nchunks;
+    if (cb && !h->prog_host) {
+        HIPC(hipHostMalloc((void**)&h->prog_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPC(hipHostGetDevicePointer((void**)&h->prog_dev, h->prog_host, 0));
+    }
+    if (cb) __atomic_store_n(h->prog_host, 0u, __ATOMIC_RELAXED);
+    a.progress = ag.progress = ar.progress = cb ? h->prog_dev : nullptr;
     for (auto e : h->pev) (void)hipEventDestroy(e);
     h->pev.clear();
     h->pev_steps.clear();
-    if (h->timing) CHECK(P.stamps.alloc((size_t)nl * 2 * sizeof(uint32_t)));
+    if (h->timing) CHECK(P.stamps.alloc((size_t)nb * 2 * sizeof(uint32_t)));
     const auto t_start = std::chrono::steady_clock::now();
-    std::vector<hipEvent_t> done(nl, nullptr);
-    // progress in reference units: step i of S, scaled over the batches
-    auto report = [&](int l) -> int {
-        (void)hipEventSynchronize(done[l]);
-        const int b = l / nchunks, i = ((l % nchunks) * G + (long long)b * S) / nb;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-        if (cb(user, i, S, B, ((long long)b * S + (l % nchunks) * G + 1) / std::max(el, 1e-9) * (B / nb) / 1000.0))
-            return fail(WRNN_ERR_ABORTED, "aborted by progress callback");
-        return WRNN_OK;
-    };
-    int rc = WRNN_OK;
-    for (int l = 0; l < nl && rc == WRNN_OK; ++l) {
-        const int b = l / nchunks, c = l % nchunks;
+    for (int b = 0; b < nb; ++b) {
         a.rb = b * kPG * a.nr;
-        a.t0 = c * G;
-        a.t1 = std::min(S, a.t0 + G);
-        if (c == 0) {
-            HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
-            HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
-        }
-        // registration words only: an error code from an earlier launch stays visible
+        a.t0 = 0;
+        a.t1 = S;
+        a.prog_base = b * S;
+        HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
+        HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
+        // registration words only: an error code from an earlier launch stays visible, so the
+        // later launches of a failed call exit at registration (p_register)
         HIPC(hipMemsetAsync(P.ctl.p, 0, PC_ERR * sizeof(unsigned), st));
-        a.stamps = h->timing ? (uint32_t*)P.stamps.p + 2 * l : nullptr;
+        a.stamps = h->timing ? (uint32_t*)P.stamps.p + 2 * b : nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->timing) {
             HIPC(hipEventCreate(&e0));
             HIPC(hipEventCreate(&e1));
             h->pev.push_back(e0);
             h->pev.push_back(e1);
-            h->pev_steps.push_back(a.t1 - a.t0);
+            h->pev_steps.push_back(S);
             HIPC(hipEventRecord(e0, st));
         }
         if (gen) {
@@ -1660,6 +1660,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ag.nr = a.nr;
             ag.rb = a.rb;
             ag.stamps = a.stamps;
+            ag.prog_base = a.prog_base;
             HIPC(launch_persist_gen(ag, st));
         } else if (rr) {
             ar.t0 = a.t0;
@@ -1667,27 +1668,49 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.nr = a.nr;
             ar.rb = a.rb;
             ar.stamps = a.stamps;
+            ar.prog_base = a.prog_base;
             HIPC(launch_persist_rr(ar, st));
         } else {
             HIPC(launch_persist(a, st));
         }
         if (h->timing) HIPC(hipEventRecord(e1, st));
-        if (cb) {
-            if (hipEventCreateWithFlags(&done[l], hipEventDisableTiming) != hipSuccess ||
-                hipEventRecord(done[l], st) != hipSuccess) {
-                rc = fail(WRNN_ERR_HIP, "event record");
-                break;
-            }
-            if (l >= 1) rc = report(l - 1);  // one launch stays queued ahead
-        }
     }
-    if (rc == WRNN_OK && cb) rc = report(nl - 1);
-    for (auto e : done)
-        if (e) (void)hipEventDestroy(e);
-    if (rc) return rc;
     unsigned err = 0;
     HIPC(hipMemcpyAsync(&err, (unsigned*)P.ctl.p + PC_ERR, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    int rc = WRNN_OK;
+    if (cb) {
+        // report i = 0, 100, 200, ... < S in order, each once, when every row has finished step i
+        // (reference units: nb row batches of S steps make S steps of all B rows)
+        hipEvent_t fin = nullptr;
+        HIPC(hipEventCreateWithFlags(&fin, hipEventDisableTiming));
+        if (hipEventRecord(fin, st) != hipSuccess) {
+            (void)hipEventDestroy(fin);
+            return fail(WRNN_ERR_HIP, "event record");
+        }
+        long long next = 0;
+        while (rc == WRNN_OK && next < S) {
+            const hipError_t q = hipEventQuery(fin);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                rc = fail(WRNN_ERR_HIP, std::string("persistent launch: ") + hipGetErrorString(q));
+                break;
+            }
+            const bool finished = q == hipSuccess;
+            if (finished && err) break;  // failed launch: no progress to report
+            const long long done = finished ? (long long)nb * S
+                                            : (long long)__atomic_load_n(h->prog_host, __ATOMIC_RELAXED);
+            const long long i_done = done / nb;  // steps every row has completed
+            while (rc == WRNN_OK && next < S && next + 1 <= i_done) {
+                const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+                if (cb(user, (int)next, S, B, (double)(next + 1) / std::max(el, 1e-9) * B / 1000.0))
+                    rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+                next += kProgressEvery;
+            }
+            if (!finished && next < S) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        (void)hipEventDestroy(fin);
+    }
     HIPC(hipStreamSynchronize(st));
+    if (rc) return rc;
     if (err) {
         static const char* what[] = {"", "workgroups did not become co-resident",
                                      "exchange timeout", "workgroups not spread 32 per XCD"};
@@ -1797,7 +1820,9 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         else if ((double)S * kPG * nr * nbatch * (4 * h->H + h->n_classes) * 4.0 > kPersistWsBytes)
             why = "P1 / noise workspace for " + std::to_string(B) + " rows x " + std::to_string(S) +
                   " steps exceeds " + std::to_string((long long)(kPersistWsBytes / (1 << 30))) + " GiB";
-        else if (h->persist_failed) why = "a persistent launch failed earlier on this handle";
+        else if (h->persist_failed && want != WRNN_ENGINE_PERSIST)
+            why = "persistent launches failed " + std::to_string(kPersistMaxStreak) +
+                  " calls in a row on this handle (" + h->fallback_reason + ")";
         else if (S >= (1 << 21)) why = "seq_len >= 2^21 (step tags)";
         else if (!persist_device_ok(h)) why = "device is not a 256-CU gfx950";
         else use_p = true;
@@ -1854,11 +1879,21 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     int rc = WRNN_OK;
     if (use_p) {
         rc = run_persist(h, S, cb, user);
+        if (rc == kPersistFallback && want == WRNN_ENGINE_PERSIST) {
+            // the caller asked for PERSIST explicitly: report, never substitute another engine
+            ++h->persist_fail_streak;
+            (void)hipStreamSynchronize(h->stream);
+            return WRNN_ERR_HIP;  // g_err: "persistent launch: ..."
+        }
         if (rc == kPersistFallback) {
-            // the persistent launch could not run (e.g. CUs unavailable): same call on CHAIN
-            std::fprintf(stderr, "[wavernn-mi355x] persist engine failed (%s); using the chain engine\n",
-                         g_err.c_str());
-            h->persist_failed = true;
+            // the persistent launch could not run (e.g. CUs unavailable): same call on CHAIN,
+            // counted (wrnn_fallback_info) and warned; AUTO keeps trying PERSIST on later calls
+            // until kPersistMaxStreak calls in a row have failed
+            ++h->fallbacks;
+            h->fallback_reason = g_err;
+            h->persist_failed = ++h->persist_fail_streak >= kPersistMaxStreak;
+            std::fprintf(stderr, "[wavernn-mi355x] WARNING: persist engine failed (%s); this call runs on the "
+                                 "chain engine (~14x slower)\n", g_err.c_str());
             use_p = false;
             if (h->pw.p1x4)  // cI was not written (P1 carried it): conditioning again, cI only
                 for (int u = 0; u < n_utts; ++u)
@@ -1876,6 +1911,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         return rc;
     }
     h->last_engine = use_p ? WRNN_ENGINE_PERSIST : WRNN_ENGINE_CHAIN;
+    if (use_p) h->persist_fail_streak = 0;
     if (seq_len) *seq_len = S;
     h->stream_ctr += (uint32_t)n_utts;
     return WRNN_OK;
@@ -2165,6 +2201,17 @@ int wrnn_set_engine(wrnn_handle* h, int engine) {
 int wrnn_last_engine(wrnn_handle* h, int* engine) {
     if (!h || !engine) return fail(WRNN_ERR_INVALID, "null argument");
     *engine = h->last_engine;
+    return WRNN_OK;
+}
+
+int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_cap) {
+    if (!h || !count) return fail(WRNN_ERR_INVALID, "null argument");
+    *count = h->fallbacks;
+    if (reason && reason_cap) {
+        const size_t n = std::min(reason_cap - 1, h->fallback_reason.size());
+        std::memcpy(reason, h->fallback_reason.data(), n);
+        reason[n] = 0;
+    }
     return WRNN_OK;
 }
 

@@ -166,6 +166,8 @@ constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
 // control words (zeroed by the host before every launch); PC_ERR: 1 registration timeout,
 // 2 exchange timeout, 3 workgroups not spread 32 per XCD
 enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WORDS = 16 };
+// progress cadence of the reference's callback (fatchord_version.py:234: i % 100 == 0)
+constexpr int kProgressEvery = 100;
 
 struct PersistArgs {
     unsigned* ctl;          // PC_WORDS control words
@@ -199,6 +201,8 @@ struct PersistArgs {
     uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
     uint32_t* phases;       // optional: [256][kPPhases] stamps of step phase_t
     int phase_t;
+    unsigned* progress;     // optional host-mapped word: steps done (persist_common.h p_progress)
+    int prog_base;          // row batch * S
 };
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
@@ -245,6 +249,8 @@ struct PersistRRArgs {
     int ld;
     float* st;              // chunk state [B][11 H]: x1, h1, h2, h3, h4 | gh2, gh3 (3H each)
     uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
+    unsigned* progress;     // as PersistArgs
+    int prog_base;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
@@ -279,6 +285,8 @@ struct PersistGenArgs {
     int ld;
     float* st;              // chunk state [B][2 H]: x1, h1
     uint32_t* stamps;
+    unsigned* progress;     // as PersistArgs
+    int prog_base;
 };
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s);

@@ -36,7 +36,7 @@ EXPORTED = [
     'wrnn_generate', 'wrnn_generate_batch_device', 'wrnn_enable_stage_timing',
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
-    'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble',
+    'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
 ]
 
 
@@ -107,6 +107,7 @@ def load_library(path=None):
                                                P(c_int), P(c_int), PROGRESS_FN, c_void_p]),
         'wrnn_set_engine': (c_int, [c_void_p, c_int]),
         'wrnn_last_engine': (c_int, [c_void_p, P(c_int)]),
+        'wrnn_fallback_info': (c_int, [c_void_p, P(c_int), ctypes.c_char_p, c_size_t]),
         'wrnn_enable_stage_timing': (c_int, [c_void_p, c_int]),
         'wrnn_stage_timing': (c_int, [c_void_p, c_int, P(ctypes.c_double), P(c_int)]),
         'wrnn_stage_info': (c_int, [c_void_p, c_int, ctypes.c_char_p, c_size_t,
@@ -147,5 +148,5 @@ def check(rc, what=''):
     if rc == WRNN_ERR_OOM:
         raise MemoryError(msg)
     if rc == WRNN_ERR_ABORTED:
-        raise KeyboardInterrupt(msg)
+        raise RuntimeError(msg)
     raise RuntimeError(msg)

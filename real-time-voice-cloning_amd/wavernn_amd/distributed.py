@@ -1,19 +1,26 @@
 """Multi-GPU vocoding: independent utterances sharded over ranks (one process per GPU).
 
 The reference has no multi-device inference path; utterances are fully
-independent, so the MI355X build shards them with no data-path collective: each rank vocodes
-its shard on its own GPU as one batch of fold rows, and the only exchange is collecting the
-finished waveforms on rank 0 (one all-gather of fixed, known sizes -- RCCL over xGMI with the
-"nccl" backend, or gloo on CPU).
+independent, so the data path shards them with no collective: each rank runs the fold
+recurrence of its shard on its own GPU as one batch of fold rows. The one exchange is the
+result collection: every rank's fold-row outputs (int16 labels for RAW / BITS, float32 samples
+for MOL -- 2 or 4 bytes per row-step, ~3.5 MB for 8 x 1000-frame utterances) are gathered to
+rank ``dst`` with one ``gather`` (RCCL over xGMI with the "nccl" backend, gloo on CPU), and
+``dst`` runs the reference's f64 post-processing (cross-fade, mu-law, de-emphasis, fade;
+fatchord_version.py:238-255) for every utterance on a host thread pool. Only ``dst`` receives
+waveforms; the other ranks get None.
 
 ``shard(lengths, world)`` balances by work: every utterance costs S = target + 2*overlap
 sequential steps regardless of length, and its number of fold rows grows with length, so the
 greedy longest-first assignment balances rows per rank.
 """
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 
 def fold_rows(n_frames, target, overlap, hop=200):
+    """num_folds of fold_with_overlap (fatchord_version.py:316-327) for an n_frames mel."""
     L = n_frames * hop
     nf = (L - overlap) // (target + overlap)
     if L - (nf * (overlap + target) + overlap) != 0:
@@ -35,13 +42,16 @@ def shard(n_frames, world, target, overlap, hop=200):
     return out
 
 
-def infer_waveforms(mels, vocode_fn, target, overlap, hop=200, device=None):
+def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, device=None,
+                    dst=0, threads=8):
     """Vocode a list of mels across the ranks of the default process group.
 
-    ``vocode_fn(list_of_mels) -> list_of_f64_waveforms`` runs on this rank (the GPU model's
-    ``generate_batch`` in production). Every rank receives the full list of waveforms in the
-    input order. Waveform lengths are known from the mel lengths, so the gather is one
-    fixed-size all-gather of padded float64 tensors.
+    ``rows_fn(list_of_mels) -> (rows, row_offsets)``: this rank's fold recurrence, ``rows`` a
+    (n_rows, seq_len) int16 / float32 tensor on ``device`` (``WaveRNN.generate_batch_device``
+    in production), ``row_offsets`` the first row of each utterance (+ the end).
+    ``post_fn(rows_np, n_frames) -> f64 waveform``: the host post-processing of one utterance
+    (``WaveRNN.postprocess_rows``). Returns the waveforms in input order on ``dst`` (None on
+    the other ranks; every waveform on a single process).
     """
     import torch
     import torch.distributed as dist
@@ -49,22 +59,41 @@ def infer_waveforms(mels, vocode_fn, target, overlap, hop=200, device=None):
     rank = dist.get_rank() if dist.is_initialized() else 0
     frames = [int(m.shape[-1]) for m in mels]
     plan = shard(frames, world, target, overlap, hop)
+    rows_of = [sum(fold_rows(frames[i], target, overlap, hop) for i in p) for p in plan]
     mine = plan[rank]
-    wavs = vocode_fn([mels[i] for i in mine]) if mine else []
+    if mine:
+        rows, roff = rows_fn([mels[i] for i in mine])
+    else:
+        rows, roff = None, [0]
     if world == 1:
-        return wavs
-    lens = [(t - 1) * hop for t in frames]
-    slots = max(len(p) for p in plan)
-    width = max(lens)
-    dev = device if device is not None else torch.device('cpu')
-    buf = torch.zeros((slots, width), dtype=torch.float64, device=dev)
-    for j, w in enumerate(wavs):
-        buf[j, :len(w)] = torch.from_numpy(np.asarray(w, dtype=np.float64))
-    bufs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf)
-    out = [None] * len(mels)
+        host = rows.cpu().numpy()
+        with ThreadPoolExecutor(threads) as ex:
+            return list(ex.map(lambda j: post_fn(host[roff[j]:roff[j + 1]], frames[mine[j]]),
+                               range(len(mine))))
+    # one gather of equal-shaped buffers (rows padded to the largest shard) to dst
+    width = max(rows_of)
+    dtype = rows.dtype if rows is not None else torch.int16
+    dev = device if device is not None else (rows.device if rows is not None else torch.device('cpu'))
+    buf = torch.zeros((width, seq_len), dtype=dtype, device=dev)
+    if rows is not None:
+        buf[:rows.shape[0]] = rows
+    # as bytes: RCCL / NCCL and gloo have no int16 type
+    wire = buf.view(torch.uint8)
+    bufs = [torch.empty_like(wire) for _ in range(world)] if rank == dst else None
+    dist.gather(wire, bufs, dst=dst)
+    if rank != dst:
+        return None
+    jobs = []
     for r in range(world):
-        host = bufs[r].cpu().numpy()
-        for j, i in enumerate(plan[r]):
-            out[i] = host[j, :lens[i]].copy()
+        host = bufs[r].view(dtype).cpu().numpy()
+        at = 0
+        for i in plan[r]:
+            nf = fold_rows(frames[i], target, overlap, hop)
+            jobs.append((i, host[at:at + nf]))
+            at += nf
+    out = [None] * len(mels)
+    with ThreadPoolExecutor(threads) as ex:
+        for i, w in zip([j[0] for j in jobs],
+                        ex.map(lambda j: post_fn(j[1], frames[j[0]]), jobs)):
+            out[i] = w
     return out

@@ -15,6 +15,7 @@ import ctypes
 import os
 import sys
 import time
+import warnings
 
 import numpy as np
 
@@ -32,6 +33,24 @@ _MODEL_IDS = {MODEL_TYPE_FATCHORD: _abi.WRNN_MODEL_FATCHORD,
 def _progbar(i, n, size=16):
     done = (i * size) // n
     return ''.join('█' if j <= done else '░' for j in range(size))
+
+
+def _wrap_callback(progress_callback):
+    """ctypes callback around the user's progress_callback: an exception it raises stops the
+    call (non-zero return -> WRNN_ERR_ABORTED) and is re-raised by the caller afterwards
+    (``err[0]``), as the reference's generate() would propagate it."""
+    err = [None]
+    if progress_callback is None:
+        return _abi.PROGRESS_FN(), err
+
+    def _cb(user, i, seq_len, b_size, rate):
+        try:
+            progress_callback(i, seq_len, b_size, rate)
+        except BaseException as e:  # noqa: B902 -- surfaced after the native call
+            err[0] = e
+            return 1
+        return 0
+    return _abi.PROGRESS_FN(_cb), err
 
 
 def _to_numpy_f32(x):
@@ -171,6 +190,20 @@ class WaveRNN:
         _abi.check(self._lib.wrnn_last_engine(self._h, ctypes.byref(e)))
         return {v: k for k, v in _abi.ENGINES.items()}[e.value]
 
+    def fallback_info(self):
+        """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
+        n = ctypes.c_int()
+        why = ctypes.create_string_buffer(256)
+        _abi.check(self._lib.wrnn_fallback_info(self._h, ctypes.byref(n), why, 256))
+        return n.value, why.value.decode('utf-8', 'replace')
+
+    def _warn_fallback(self, before):
+        n, why = self.fallback_info()
+        if n > before:
+            warnings.warn(f'WaveRNN (MI355X): the persistent engine could not run ({why}); this '
+                          f'call ran on the chain engine (~14x slower)', RuntimeWarning,
+                          stacklevel=3)
+
     def enable_stage_timing(self, enable=True):
         _abi.check(self._lib.wrnn_enable_stage_timing(self._h, int(bool(enable))))
 
@@ -229,20 +262,9 @@ class WaveRNN:
         n = B * S
         labels = np.empty((B, S), dtype=np.int16) if self.categorical else None
         samples = None if self.categorical else np.empty((B, S), dtype=np.float32)
-        cb_ref = [None]
-
-        if progress_callback is not None:
-            def _cb(user, i, seq_len, b_size, rate):
-                try:
-                    progress_callback(i, seq_len, b_size, rate)
-                except Exception as e:  # surface callback errors after the call
-                    cb_ref[0] = e
-                    return 1
-                return 0
-            cfn = _abi.PROGRESS_FN(_cb)
-        else:
-            cfn = _abi.PROGRESS_FN()
+        cfn, cb_ref = _wrap_callback(progress_callback)
         ob, os_ = ctypes.c_int(), ctypes.c_int()
+        fb0 = self.fallback_info()[0]
         rc = self._lib.wrnn_generate(
             self._h, mel.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), T,
             int(bool(batched)), int(target or 0), int(overlap or 0),
@@ -252,6 +274,7 @@ class WaveRNN:
         if cb_ref[0] is not None:
             raise cb_ref[0]
         _abi.check(rc, 'generate')
+        self._warn_fallback(fb0)
         if labels is not None:
             samples = labels_to_samples(labels, self.n_classes)
         return labels, samples, B, S
@@ -287,14 +310,16 @@ class WaveRNN:
             lab_p, smp_p = None, out.data_ptr()
         roff = (ctypes.c_int * (n + 1))()
         s_out = ctypes.c_int()
-        cfn = _abi.PROGRESS_FN()
-        if progress_callback is not None:
-            cfn = _abi.PROGRESS_FN(lambda u, i, sl, b, r: (progress_callback(i, sl, b, r), 0)[1])
+        cfn, cb_ref = _wrap_callback(progress_callback)
         torch.cuda.current_stream(dev).synchronize()
+        fb0 = self.fallback_info()[0]
         rc = self._lib.wrnn_generate_batch_device(
             self._h, n, ptrs, frames, int(bool(batched)), int(target or 0), int(overlap or 0),
             lab_p, smp_p, rows * S, roff, ctypes.byref(s_out), cfn, None)
+        if cb_ref[0] is not None:
+            raise cb_ref[0]
         _abi.check(rc, 'generate_batch_device')
+        self._warn_fallback(fb0)
         return out, list(roff), S
 
     def generate_batch(self, mels_dev, batched, target, overlap, mu_law, apply_preemphasis,
@@ -304,21 +329,26 @@ class WaveRNN:
         out, roff, S = self.generate_batch_device(mels_dev, batched, target, overlap,
                                                   progress_callback)
         host = out.cpu().numpy()
-        wavs = []
-        for u, m in enumerate(mels_dev):
-            rows = host[roff[u]:roff[u + 1]]
-            wave_len = (int(m.shape[-1]) - 1) * self.hop_length
-            if self.categorical and batched:
-                wav = postprocess_labels(rows, target, overlap, mu_law, apply_preemphasis,
-                                         self.n_classes, wave_len, self.hop_length, self._lib)
-                if wav is not None:
-                    wavs.append(wav)
-                    continue
-            smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
-            wavs.append(postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
-                                    self.n_classes, wave_len, self.hop_length,
-                                    labels=rows if self.categorical else None, lib=self._lib))
-        return wavs
+        self.last_batch_rows, self.last_batch_offsets = host, roff
+        return [self.postprocess_rows(host[roff[u]:roff[u + 1]], int(m.shape[-1]), batched,
+                                      target, overlap, mu_law, apply_preemphasis)
+                for u, m in enumerate(mels_dev)]
+
+    def postprocess_rows(self, rows, n_frames, batched, target, overlap, mu_law,
+                         apply_preemphasis):
+        """Host f64 post-processing of one utterance's fold rows (fatchord_version.py:238-255):
+        ``rows`` (num_folds, S) int16 labels (categorical) or float32 samples (MOL)."""
+        mu_law = mu_law if self.mode == 'RAW' else False
+        wave_len = (int(n_frames) - 1) * self.hop_length
+        if self.categorical and batched:
+            wav = postprocess_labels(rows, target, overlap, mu_law, apply_preemphasis,
+                                     self.n_classes, wave_len, self.hop_length, self._lib)
+            if wav is not None:
+                return wav
+        smp = labels_to_samples(rows, self.n_classes) if self.categorical else rows
+        return postprocess(smp, batched, target, overlap, mu_law, apply_preemphasis,
+                           self.n_classes, wave_len, self.hop_length,
+                           labels=rows if self.categorical else None, lib=self._lib)
 
     def generate(self, mels, batched, target, overlap, mu_law, apply_preemphasis,
                  progress_callback=None):

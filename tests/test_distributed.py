@@ -1,7 +1,10 @@
 """Multi-process path (CPU, gloo, world_size 2): utterance sharding + result collection.
 
-The per-rank vocoder here is the oracle on tiny inputs (test infrastructure); on the GPU box
-the same infer_waveforms() drives WaveRNN.generate_batch with the nccl (RCCL) backend.
+The per-rank fold recurrence here is the oracle on tiny inputs (test infrastructure) and the
+host post-processing is the product's (wavernn_amd.audio with the C-ABI library's host loops);
+int16 labels are gathered to rank 0, which post-processes every utterance. On the GPU box
+bench.py --gpus N drives the same infer_waveforms() with WaveRNN.generate_batch_device on the
+nccl (RCCL) backend.
 """
 import os
 import socket
@@ -42,19 +45,31 @@ def _worker(rank, world, port, q):
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from oracle.wavernn_oracle import oracle_infer_waveform
+    from wavernn_amd import _abi
+    from wavernn_amd.audio import postprocess
     from wavernn_amd.distributed import infer_waveforms
     from wavernn_amd.hparams import wavernn_fatchord
     from wavernn_amd.synth import synth_state_dict, synth_mel
     hp = wavernn_fatchord.copy(bits=9)
     sd = synth_state_dict(hp, 'fatchord-wavernn', seed=1)
     mels = [synth_mel(T, seed=10 + i) for i, T in enumerate([22, 30, 25])]
+    lib = _abi.load_library()
 
-    def vocode(ms):
-        return [oracle_infer_waveform(sd, hp, 'fatchord-wavernn', m, target=400, overlap=50,
-                                      seed=5, stream=0)['wav'] for m in ms]
-    wavs = infer_waveforms(mels, vocode, 400, 50)
+    def rows_fn(ms):
+        outs = [oracle_infer_waveform(sd, hp, 'fatchord-wavernn', m, target=400, overlap=50,
+                                      seed=5, stream=0, post=False)['labels'] for m in ms]
+        roff = np.cumsum([0] + [o.shape[0] for o in outs]).tolist()
+        return torch.from_numpy(np.concatenate(outs)), roff
+
+    def post_fn(rows, n_frames):
+        smp = (np.float32(2) * rows.astype(np.float32)) / np.float32(511.) - np.float32(1.)
+        return postprocess(smp, True, 400, 50, True, True, 512, (n_frames - 1) * 200, 200,
+                           labels=rows, lib=lib)
+    wavs = infer_waveforms(mels, rows_fn, post_fn, 400, 50, seq_len=500)
     if rank == 0:
         q.put([w.tolist() for w in wavs])
+    else:
+        assert wavs is None
     dist.destroy_process_group()
 
 

@@ -1,0 +1,94 @@
+"""progress_callback contract of WaveRNN.generate on both engines.
+
+Reference: fatchord_version.py:234-236 calls ``progress_callback(i, seq_len, b_size, gen_rate)``
+when ``i % 100 == 0`` -- so i = 0, 100, ..., in order, once each, b_size = number of fold rows.
+On PERSIST the kernels publish their step count to host-mapped memory and the host reports from
+it while one launch per row batch runs all steps (the callback no longer splits launches).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(name):
+    from test_gpu_parity import make_model
+    meta, gold = golden_case(name)
+    m, hp, sd = make_model(meta)
+    return meta, gold, m, hp
+
+
+@pytest.mark.parametrize('engine', ['persist', 'chain'])
+def test_callback_sequence_single_utterance(engine):
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold, m, hp = _model('fatchord_raw9_config1')
+    m.set_engine(engine)
+    calls = []
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    wav = m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+                     progress_callback=lambda *c: calls.append(c))
+    assert m.last_engine() == engine
+    S, B = meta['seq_len'], meta['num_folds']
+    assert [c[0] for c in calls] == list(range(0, S, 100))
+    assert all(c[1] == S and c[2] == B and c[3] > 0 for c in calls)
+    assert np.array_equal(wav, gold['wav'])
+
+
+def test_callback_sequence_over_row_batches():
+    """40 rows -> several persistent row batches: still i = 0, 100, ... < S exactly once."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold, m, hp = _model('fatchord_raw9_tiny')
+    m.set_engine('persist')
+    mels = [torch.from_numpy((synth_mel(meta['n_frames'], 300 + u) / sp.max_abs_value)
+                             .astype(np.float32)).cuda() for u in range(8)]
+    calls = []
+    out, roff, S = m.generate_batch_device(mels, True, meta['target'], meta['overlap'],
+                                           progress_callback=lambda *c: calls.append(c))
+    assert m.last_engine() == 'persist'
+    assert [c[0] for c in calls] == list(range(0, S, 100))
+    assert all(c[1] == S and c[2] == roff[-1] for c in calls)
+
+
+@pytest.mark.parametrize('engine', ['persist', 'chain'])
+def test_callback_exception_propagates(engine):
+    """An exception raised by the callback reaches the caller (as it would from the reference's
+    Python loop) and no further callbacks run."""
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold, m, hp = _model('fatchord_raw9_tiny')
+    m.set_engine(engine)
+    calls = []
+
+    class Stop(Exception):
+        pass
+
+    def cb(i, *a):
+        calls.append(i)
+        if i >= 200:
+            raise Stop()
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    with pytest.raises(Stop):
+        m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+                   progress_callback=cb)
+    assert calls == [0, 100, 200]
+    # the handle stays usable
+    m.set_seed(meta['noise_seed'])
+    wav = m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+                     progress_callback=lambda *a: None)
+    assert np.array_equal(wav, gold['wav'])
+
+
+def test_no_fallback_recorded():
+    meta, gold, m, hp = _model('fatchord_raw9_tiny')
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+               progress_callback=lambda *a: None)
+    assert m.last_engine() == 'persist'
+    assert m.fallback_info()[0] == 0
