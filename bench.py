@@ -110,9 +110,9 @@ def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0):
 def _bounded_leg(args, sd, hp, mel, threads, seconds):
     """Oracle on `threads` host threads: upsample + the first k steps (k sized to ~seconds),
     the loop time extrapolated to all S steps."""
-    probe = _oracle_run(args, sd, hp, mel, threads, max_steps=20)
-    per_step = probe['t_loop'] / 20
-    k = int(max(50, min(probe['S'], seconds / max(per_step, 1e-6))))
+    probe = _oracle_run(args, sd, hp, mel, threads, max_steps=5)
+    per_step = probe['t_loop'] / 5
+    k = int(max(5, min(probe['S'], seconds / max(per_step, 1e-6))))
     r = _oracle_run(args, sd, hp, mel, threads, max_steps=k)
     t_total = r['t_prepare'] + r['t_loop'] * r['S'] / r['steps']
     samples = (args.frames - 1) * 200
