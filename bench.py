@@ -79,10 +79,18 @@ CU_FP32_FLOP_PER_US = 64 * 4 * 2400.0
 PERSIST_HOPS = {'fatchord-wavernn': 4, 'runtimeracer-wavernn': 8, 'geneing-wavernn': 2}
 
 
-def latency_floor_us(model_type, hp, rows_per_group, n_classes):
-    """Lower bound of one persistent step: exchange hops + critical products of one slot."""
+# MACs per row-step of the recurrent weight matrices
+MACS_PER_ROW_STEP = {'fatchord-wavernn': 4071424, 'runtimeracer-wavernn': 2035712}
+
+
+def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False):
+    """Lower bound of one persistent step: exchange hops + critical products of one slot.
+    Wide launches (kernels_persist_wide.hip) have one more hop (GRU1 is distributed) and run
+    the products on 16-column MFMA tiles: 16 rows of work whatever the row count."""
     H, F = hp.rnn_dims, hp.fc_dims
     slots = 32
+    if wide:
+        rows_per_group = 16
     if model_type == 'fatchord-wavernn':      # GRU2 (3H x H) -> fc1 -> fc2 -> fc3
         crit = 3 * H * H + F * H + F * F + n_classes * F
     elif model_type == 'runtimeracer-wavernn':  # GRU2, GRU3, GRU4, fc1..fc5
@@ -90,7 +98,7 @@ def latency_floor_us(model_type, hp, rows_per_group, n_classes):
     else:                                       # geneing: fc1 -> fc3
         crit = F * H + n_classes * F
     flop = 2.0 * crit * rows_per_group / slots
-    hops = PERSIST_HOPS[model_type]
+    hops = PERSIST_HOPS[model_type] + (1 if wide else 0)
     return hops * HANDOFF_US + flop / CU_FP32_FLOP_PER_US, hops
 
 
@@ -250,7 +258,7 @@ def main():
         dom = max(info, key=lambda r: (r[3] if r[3] == r[3] else 0) * r[4])
         name, by, fl, us, n = dom
         achieved = by / (us * 1e-6) / 1e9 if us > 0 else None
-        kernel = 'k_persist' if name == 'persist' else f'k_stage<{name}>'
+        kernel = {'persist': 'k_persist', 'persist_wide': 'k_persist_wide'}.get(name, f'k_stage<{name}>')
         roof = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': None,
@@ -259,11 +267,13 @@ def main():
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
                 'fp32_frac': fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
-        if name == 'persist':  # one launch per row batch runs all S steps
+        if name in ('persist', 'persist_wide'):  # one launch per row batch runs all S steps
             roof['us_per_step'] = us / S
-            roof['launches_per_generate'] = n  # stage timing keeps the last generate's launches
-            nr = -(-rows_per_gpu // (8 * n)) if n else 0
-            floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes)
+            roof['launches_per_generate'] = sum(r[4] for r in info)
+            rows_l = fl / (S * 2.0 * MACS_PER_ROW_STEP.get(args.model, 1)) if S else 0
+            nr = -(-int(round(rows_l)) // 8)
+            floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes,
+                                           wide=name == 'persist_wide')
             roof['latency_floor_us'] = floor
             roof['latency_frac'] = floor / roof['us_per_step']
             roof['latency_model'] = (f'{hops} in-group hops x {HANDOFF_US} us (handoff-1to1) + '

@@ -1,0 +1,524 @@
+// Persistent fatchord recurrence for WIDE row batches (the "persist-wide" launch kind):
+// up to 16 fold rows per XCD group, 128 rows per launch, the matrix-vector products of every
+// step on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact f32, the fp32 vector rate).
+//
+// Reference step body: vocoder/models/fatchord_version.py:192-236 (same restructuring as
+// kernels_persist.hip: conditioning hoisted into per-frame / per-step precomputes, torch
+// GRUCell arithmetic). What changes at 16 rows per group:
+//  * Products as MFMA tiles. A workgroup (slot w of its XCD group) owns units / outputs
+//    [16w, 16w + 16) of every layer and classes [16w, 16w + 16) of fc3: one 16-row M tile per
+//    gate matrix. The group's rows are the 16 N columns. K = 512 is split over the 8 waves
+//    (wave v: units [64v, 64v + 64), 16 k-steps of 4); the 8 partial tiles are summed in LDS in
+//    a fixed order (deterministic). Weights stay resident: 10 tiles per wave in registers
+//    (W_ih2[:, :512] r/z/n, W_hh1 r/z/n, fc1, fc2, fc3), W_hh2 r/z/n in LDS.
+//  * GRU1 distributed, not redundant: each slot runs GRU1 for its own 16 units x rows and
+//    publishes x1 / h1 (redundant GRU1 of all 512 units would cost 16x the cell work here).
+//    Five in-group hops per step: E (x1, h1), A (x2, h2), B (y1), C (y2), D (fc3 candidates).
+//  * Exchange: every published vector is laid out as 16-byte couples {v(u), tag, v(u+1), tag}
+//    in MFMA B-operand order ([wave e][couple i][k-slot c][row n]), so a consumer wave reads its
+//    B operand straight into registers with 8 fully coalesced 1-KiB loads per hop and checks
+//    the step tags itself -- no LDS staging of activations, no flags. Producers store with
+//    plain vector stores; consumers load non-temporal (L2-served): both ends of every hop are
+//    on one XCD (HW_REG_XCC_ID grouping), so the XCD's L2 is the coherence point (DESIGN.md §3,
+//    "Memory ordering").
+//  * Off-path products (W_hh1 h1 -> gh1, W_hh2 h2 -> gh2 of the next step) run in the waits of
+//    hops A and B; waves 4-7 (no epilogue cells) start them while waves 0-3 run the epilogues.
+// Every spin is bounded; on a timeout / error the kernel sets PC_ERR and every wave exits at
+// its next barrier.
+#include "wrnn_kernels.h"
+#include "persist_common.h"
+
+namespace wrnn {
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// ---- exchange area per group (floats) ---------------------------------------------------
+constexpr int WV = 8 * 8 * 4 * 16 * 4;  // one vector buffer: [e 8][i 8][c 4][n 16] couples
+enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
+constexpr int WX_D = WB_N * WV;                    // candidates [n 16][slot 32] (value, tag|class)
+constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
+
+// ---- LDS (floats) -------------------------------------------------------------------------
+// Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
+// the instruction's 16-bit immediate (beyond it each access would pin an address register).
+constexpr int WL_GH1 = 0;                        // gh1 of the slot's units [3][16 n][16 ul]
+constexpr int WL_GH2 = WL_GH1 + 768;             // gh2 [3][16 n][16 ul]
+constexpr int WL_X1 = WL_GH2 + 768;              // x1 of the slot's units [16 n][16 ul]
+constexpr int WL_SX = WL_X1 + 256;               // sample per row [16]
+constexpr int WL_CV = WL_SX + 16;                // hop-D partial argmax [4][16] value, class
+constexpr int WL_CI = WL_CV + 64;
+constexpr int WL_RI = WL_CI + 64;                // RowInfo of the group's rows (6 words each)
+constexpr int WL_FAIL = WL_RI + 16 * 6;
+constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
+constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
+constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
+constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
+constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
+constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
+constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
+static_assert(WL_REG + 4 <= WL_PS, "small LDS arrays overflow their 8 KiB");
+static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
+static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
+static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
+
+// register tiles of a wave: 0-2 W_ih2x r,z,n | 3-5 W_hh1 r,z,n | 6 fc1 | 7 fc2 | 8 fc3
+constexpr int kWTiles = 9;
+
+__device__ __forceinline__ v4f mfma4(float a, float b, v4f c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float f4c(const float4& q, int i) {
+    return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w;
+}
+// B operand of k-step ks from the 8 couples of a hop (couple i holds k-steps 2i, 2i + 1)
+__device__ __forceinline__ float bop(const u4v (&cc)[8], int ks) {
+    return __uint_as_float((ks & 1) ? cc[ks >> 1].z : cc[ks >> 1].x);
+}
+
+// LDS-only workgroup barrier: no wait on outstanding global loads (prefetches stay in flight)
+__device__ __forceinline__ void wbar() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Poll this lane's 8 couples of one hop buffer (byte offset of couple 0: voff; couple i at
+// voff + 1 KiB i) until all 16 tags equal `want`: spin on couple 0, then load the rest and
+// verify. Lanes with valid == false (rows beyond the group's count) contribute zeros.
+__device__ __forceinline__ bool w_poll8(rsrc_t xr, unsigned voff, unsigned so, unsigned want,
+                                        bool valid, u4v (&cc)[8], unsigned* ctl) {
+    const unsigned t0 = p_now();
+    unsigned nsp = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cc[i] = (u4v){0u, want, 0u, want};
+    while (true) {
+        if (valid) cc[0] = __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, kCpNT);
+        if (__all(cc[0].y == want && cc[0].w == want)) {
+            bool ok = true;
+            if (valid) {
+                unsigned vo = voff;
+                asm volatile("" : "+v"(vo));  // (offsets recomputed per use: hoisted ones pin registers)
+#pragma unroll
+                for (int i = 1; i < 8; ++i)
+                    cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+#pragma unroll
+                for (int i = 1; i < 8; ++i) ok = ok && cc[i].y == want && cc[i].w == want;
+            }
+            if (__all(ok)) return true;
+        }
+        if ((++nsp & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
+            if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
+            return false;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
+    int* sreg = reinterpret_cast<int*>(lds + WL_REG);
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        int gg, ss;
+        sreg[2] = p_register(a.ctl, gg, ss);
+        sreg[0] = gg;
+        sreg[1] = ss;
+    }
+    __syncthreads();
+    if (!sreg[2]) return;
+    const int g = __builtin_amdgcn_readfirstlane(sreg[0]);
+    const int w = __builtin_amdgcn_readfirstlane(sreg[1]);
+    const int v = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave: K-eighth [64v, 64v + 64)
+    const int l = tid & 63;
+    const int R = a.nr;                  // rows of this group (<= 16)
+    const int g0 = a.rb + g;             // group row r = fold row g0 + 8 r
+    const int bn = l & 15;               // B-operand lane: row bn, k-slot l >> 4
+    const bool bvalid = bn < R;
+    // epilogue cell of threads 0..16R-1: row cn, unit / class 16 w + cul
+    const int cn = tid >> 4, cul = tid & 15;
+    const bool cell = tid < 16 * R;
+    const int cu = 16 * w + cul;
+    const int crow = g0 + kPG * (cell ? cn : 0);
+    const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * WX_GROUP);
+    const bool trace = a.phases != nullptr;
+    uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
+#define WSTAMP(i) \
+    if (trace && t == a.phase_t && (tid & 255) == 0) ph[(tid >> 8) * 12 + (i)] = p_now();
+
+    // ---- weights ------------------------------------------------------------------------
+    float4 wq[4 * kWTiles];  // tile T, k-step ks: wq[4T + ks / 4] component ks % 4
+    {
+        const float4* src = a.wwide + ((size_t)(w * 8 + v) * 4 * kWTiles) * 64 + l;
+#pragma unroll
+        for (int q = 0; q < 4 * kWTiles; ++q) wq[q] = src[(size_t)q * 64];
+        const float4* hs = a.wwide_lds + (size_t)w * (WL_HH2_SZ / 4);
+        float4* hd = reinterpret_cast<float4*>(lds + WL_HH2);
+        for (int i = tid; i < WL_HH2_SZ / 4; i += kPT) hd[i] = hs[i];
+    }
+#define WR(T, ks) f4c(wq[4 * (T) + (ks) / 4], (ks) % 4)
+    const float4* hh2 = reinterpret_cast<const float4*>(lds + WL_HH2);
+    // ---- state and per-cell constants --------------------------------------------------
+    float h1r = 0.f, h2r = 0.f, vj0 = 0.f, vj1 = 0.f, vj2 = 0.f, w0u = 0.f;
+    if (cell) {
+        h1r = a.st_h1[(size_t)crow * kPH + cu];
+        h2r = a.st_h2[(size_t)crow * kPH + cu];
+        lds[WL_X1 + cn * 16 + cul] = a.st_x1[(size_t)crow * kPH + cu];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            lds[WL_GH2 + (j * 16 + cn) * 16 + cul] = a.st_gh2[(size_t)crow * 3 * kPH + j * kPH + cu];
+        vj0 = a.v[cu];
+        vj1 = a.v[kPH + cu];
+        vj2 = a.v[2 * kPH + cu];
+        w0u = a.w0[cu];
+    }
+    if (tid < R) reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid == 0) lds[WL_FAIL] = 0.f;
+    // byte offsets: this lane's couple 0 in a hop buffer (consumer); the cell pair's couple
+    // (producer: even units publish the pair {u, u + 1})
+    const unsigned o_cons = (unsigned)((v * 8 * 64 + l) * 16);
+    const unsigned o_prod = (unsigned)(((((w >> 2) * 8 + (cul >> 1)) * 4 + (w & 3)) * 16 + cn) * 16);
+    auto pub = [&](int hb, float val, unsigned tag) {
+        const float nb = pdpp<0xB1>(val);  // unit u ^ 1 of the same row (quad_perm xor 1)
+        if (cell && (cul & 1) == 0)
+            __builtin_amdgcn_raw_buffer_store_b128((u4v){__float_as_uint(val), tag, __float_as_uint(nb), tag},
+                                                   xr, o_prod, (unsigned)(hb * WV) * 4u, 0);
+    };
+    const rsrc_t fcr = mk_rsrc(a.fcond);
+    // per-step operands of the cell, loaded right after the hop E poll:
+    //   pc[0..2] GRU2 cond (W_ih2[:, 512:] a2 + b_ih2), pc[3] fc1 cond, pc[4] fc2 cond (frame t)
+    //   pg       Gumbel noise of (row, class cu) at step t
+    //   pp       P1(t + 1) of (row, unit cu): r, z, n of W_ih1 I(c) + b_ih1, then cI
+    float pc[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, pg = 0.f;
+    float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto prefetch = [&](int t) {
+        if (!cell) return;
+        const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[cn];
+        const unsigned fo = (unsigned)(p_frame(ri, t, a.hop) * a.cond_width) * 4u;
+        int uu = cu;
+        asm volatile("" : "+v"(uu));  // (recomputed per step: hoisted offsets cost registers)
+        pc[0] = bld(fcr, fo + (unsigned)(a.oG2 + uu) * 4u, 0);
+        pc[1] = bld(fcr, fo + (unsigned)(a.oG2 + kPH + uu) * 4u, 0);
+        pc[2] = bld(fcr, fo + (unsigned)(a.oG2 + 2 * kPH + uu) * 4u, 0);
+        pc[3] = bld(fcr, fo + (unsigned)(a.oF1 + uu) * 4u, 0);
+        pc[4] = bld(fcr, fo + (unsigned)(a.oF2 + uu) * 4u, 0);
+        pg = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + crow) * a.n_classes), (unsigned)uu * 4u, 0);
+        const int tn = t + 1 < a.S ? t + 1 : a.S - 1;
+        pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            mk_rsrc(a.P1 + ((size_t)tn * a.B + crow) * 4 * kPH),
+                                            (unsigned)uu * 16u, 0, 0));
+    };
+    __syncthreads();
+    // initial hop E: x1, h1 of step t0 (k_persist_init) with tag t0 + 1
+    pub(WB_X1, cell ? lds[WL_X1 + cn * 16 + cul] : 0.f, (unsigned)a.t0 + 1u);
+    pub(WB_H1, h1r, (unsigned)a.t0 + 1u);
+    const unsigned so_x1 = (unsigned)(WB_X1 * WV) * 4u, so_h1 = (unsigned)(WB_H1 * WV) * 4u;
+    const unsigned so_x2 = (unsigned)(WB_X2 * WV) * 4u, so_h2 = (unsigned)(WB_H2 * WV) * 4u;
+    const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u, so_y2 = (unsigned)(WB_Y2 * WV) * 4u;
+    const bool lo = v < 4;  // waves 0-3 hold the epilogue cells
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
+    for (int t = a.t0; t < a.t1; ++t) {
+        const unsigned seq = (unsigned)t + 1u;
+        u4v cc[8];
+        bool fail = false;
+        WSTAMP(0);
+        // ================= hop E -> stage A: W_ih2[:, :512] x1 (critical) ==================
+        fail |= !w_poll8(xr, o_cons, so_x1, seq, bvalid, cc, a.ctl);
+        prefetch(t);
+        WSTAMP(1);
+        {
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const float b = bop(cc, ks);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(j, ks), b, acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
+        }
+        if (fail) lds[WL_FAIL] = 1.f;
+        wbar();
+        WSTAMP(2);
+        if (lds[WL_FAIL] != 0.f) return;
+        // ================= GRU2 epilogue (waves 0-3) -> publish x2, h2 =====================
+        if (lo) {
+            float x2 = 0.f;
+            if (cell) {
+                float gi[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + cn) * 16 + cul];
+                    gi[j] = p_add(s, pc[j]);
+                }
+                const float* gh = lds + WL_GH2 + cn * 16 + cul;
+                h2r = p_gru(gi[0], gi[1], gi[2], gh[0], gh[256], gh[512], h2r);
+                x2 = p_add(lds[WL_X1 + cn * 16 + cul], h2r);
+            }
+            pub(WB_X2, x2, seq);
+            pub(WB_H2, h2r, seq);
+        }
+        WSTAMP(3);
+        // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
+        {
+            fail |= !w_poll8(xr, o_cons, so_h1, seq, bvalid, cc, a.ctl);
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const float b = bop(cc, ks);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(3 + j, ks), b, acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PH + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
+        }
+        // ================= hop A -> stage B: fc1 x2 (critical) =============================
+        fail |= !w_poll8(xr, o_cons, so_x2, seq, bvalid, cc, a.ctl);
+        WSTAMP(4);
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(6, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(6, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + 4 * (l >> 4)) = acc0 + acc1;
+        }
+        if (fail) lds[WL_FAIL] = 1.f;
+        wbar();
+        WSTAMP(5);
+        if (lds[WL_FAIL] != 0.f) return;
+        // fc1 epilogue (waves 0-3): y1 = relu(fc1 x2 + fc1[:, 512:] a3 + b) -> publish
+        if (lo) {
+            float y = 0.f;
+            if (cell) {
+                float s = 0.f;
+#pragma unroll
+                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
+                y = p_add(s, pc[3]);
+                y = y > 0.f ? y : 0.f;
+            }
+            pub(WB_Y1, y, seq);
+        }
+        // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
+        {
+            fail |= !w_poll8(xr, o_cons, so_h2, seq, bvalid, cc, a.ctl);
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);  // one k-quad of LDS weights live at a time
+                float4 aw[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) aw[j] = hh2[((j * 8 + v) * 4 + q) * 64 + l];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float b = bop(cc, 4 * q + k);
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) acc[j] = mfma4(f4c(aw[j], k), b, acc[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
+        }
+        // ================= hop B -> stage C: fc2 y1 (critical) =============================
+        fail |= !w_poll8(xr, o_cons, so_y1, seq, bvalid, cc, a.ctl);
+        WSTAMP(6);
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(7, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(7, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + 4 * (l >> 4)) = acc0 + acc1;
+        }
+        if (fail) lds[WL_FAIL] = 1.f;
+        wbar();
+        WSTAMP(7);
+        if (lds[WL_FAIL] != 0.f) return;
+        if (lo) {  // fc2 epilogue: y2 = relu(fc2 y1 + fc2[:, 512:] a4 + b) -> publish
+            float y = 0.f;
+            if (cell) {
+                float s = 0.f;
+#pragma unroll
+                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
+                y = p_add(s, pc[4]);
+                y = y > 0.f ? y : 0.f;
+            }
+            pub(WB_Y2, y, seq);
+        } else {  // gh2 of the next step = sum of the W_hh2 h2 partials + b_hh2 (waves 4-7)
+            const int i = tid - 256, rn = i >> 4, ul = i & 15;
+            if (rn < R)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + rn) * 16 + ul];
+                    lds[WL_GH2 + (j * 16 + rn) * 16 + ul] =
+                        p_add(s, bld(mk_rsrc(a.b_hh2), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                }
+        }
+        // ================= hop C -> stage D: fc3 y2 (critical) =============================
+        fail |= !w_poll8(xr, o_cons, so_y2, seq, bvalid, cc, a.ctl);
+        WSTAMP(8);
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(8, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(8, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + 4 * (l >> 4)) = acc0 + acc1;
+        }
+        if (fail) lds[WL_FAIL] = 1.f;
+        wbar();
+        WSTAMP(9);
+        if (lds[WL_FAIL] != 0.f) return;
+        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+        if (lo) {
+            // fc3 epilogue: candidate argmax_k (l_k + g_k) over the slot's 16 classes per row
+            // (row cn = one DPP row of 16 lanes), published tagged by lane cul == 0
+            float val = -INFINITY;
+            int cls = cu;
+            if (cell && cu < a.n_classes) {
+                float s = 0.f;
+#pragma unroll
+                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
+                val = p_add(p_add(s, bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)), pg);
+            }
+            row16_argmax(val, cls);
+            if (cell && cul == 0)
+                __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls}, xr,
+                                                      (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
+        } else {  // gh1 = sum of the W_hh1 h1 partials + b_hh1 (waves 4-7)
+            const int i = tid - 256, rn = i >> 4, ul = i & 15;
+            if (rn < R)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
+                    lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
+                        p_add(s, bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                }
+        }
+        // ================= hop D: sample of step t (wave 0, every workgroup) ===============
+        if (v == 0) {
+            const int n = l & 15, gq = l >> 4;  // row n, slots 8 gq .. 8 gq + 7
+            const bool valid = n < R;
+            const unsigned off = (unsigned)((n * 32 + 8 * gq) * 2) * 4u;
+            const unsigned want = seq & kTagSeqMask;
+            u4v q[4] = {(u4v){0u, want << 11, 0u, want << 11}, (u4v){0u, want << 11, 0u, want << 11},
+                        (u4v){0u, want << 11, 0u, want << 11}, (u4v){0u, want << 11, 0u, want << 11}};
+            const unsigned t0s = p_now();
+            unsigned nsp = 0;
+            while (true) {
+                bool ok = true;
+                if (valid) {
+                    unsigned vo = off;
+                    asm volatile("" : "+v"(vo));
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        q[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, WX_D * 4 + 16u * k, kCpNT);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) ok = ok && (q[k].y >> 11) == want && (q[k].w >> 11) == want;
+                }
+                if (__all(ok)) break;
+                if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
+                    if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                    fail = true;
+                    break;
+                }
+            }
+            float bv = -INFINITY;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // slots in ascending order; ties -> lowest class
+                const float v0 = __uint_as_float(q[k].x), v1 = __uint_as_float(q[k].z);
+                const int k0 = (int)(q[k].y & 0x7ffu), k1 = (int)(q[k].w & 0x7ffu);
+                if (v0 > bv || (v0 == bv && k0 < bi)) { bv = v0; bi = k0; }
+                if (v1 > bv || (v1 == bv && k1 < bi)) { bv = v1; bi = k1; }
+            }
+            lds[WL_CV + gq * 16 + n] = bv;
+            lds[WL_CI + gq * 16 + n] = __int_as_float(bi);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (gq == 0 && valid) {
+#pragma unroll
+                for (int k = 1; k < 4; ++k) {
+                    const float v2 = lds[WL_CV + k * 16 + n];
+                    const int k2 = __float_as_int(lds[WL_CI + k * 16 + n]);
+                    if (v2 > bv || (v2 == bv && k2 < bi)) { bv = v2; bi = k2; }
+                }
+                float xv;
+                {
+#pragma clang fp contract(off)
+                    xv = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
+                }
+                lds[WL_SX + n] = xv;
+                if (w == 0) {
+                    int nn = n;
+                    asm volatile("" : "+v"(nn));
+                    const unsigned ro = (unsigned)((g0 + kPG * nn) * a.ld);
+                    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels), ro * 2u,
+                                                          (unsigned)t * 2u, 0);
+                    bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                }
+            }
+        }
+        if (fail) lds[WL_FAIL] = 1.f;
+        wbar();
+        WSTAMP(10);
+        if (lds[WL_FAIL] != 0.f) return;
+        // ================= GRU1 of step t + 1 for the slot's units -> publish x1, h1 ========
+        //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
+        // (at the last step it runs on clamped inputs and nobody reads the result)
+        if (lo) {
+            float x1 = 0.f;
+            if (cell) {
+                const float x = lds[WL_SX + cn];
+                const float* gh = lds + WL_GH1 + cn * 16 + cul;
+                h1r = p_gru(fmaf(vj0, x, pp.x), fmaf(vj1, x, pp.y), fmaf(vj2, x, pp.z), gh[0], gh[256],
+                            gh[512], h1r);
+                x1 = p_add(fmaf(w0u, x, pp.w), h1r);
+                lds[WL_X1 + cn * 16 + cul] = x1;
+            }
+            pub(WB_X1, x1, seq + 1u);
+            pub(WB_H1, h1r, seq + 1u);
+        }
+        if (g == 0 && w == 0 && tid == 0) p_progress(a.progress, a.prog_base, t);
+        WSTAMP(11);
+    }
+#undef WSTAMP
+#undef WR
+    if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+}
+
+size_t persist_wide_lds_bytes() { return (size_t)WL_TOTAL * sizeof(float); }
+size_t persist_wide_xbuf_floats() { return (size_t)kPG * WX_GROUP; }
+size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
+size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
+
+int persist_wide_scratch() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
+    if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > kPM * 16 ||
+        a.mode != 0 || a.wwide == nullptr)
+        return hipErrorInvalidValue;
+    static bool attr = false;
+    const size_t lds = persist_wide_lds_bytes();
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_wide,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_persist_wide, dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace wrnn

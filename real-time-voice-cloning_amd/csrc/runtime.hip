@@ -183,6 +183,7 @@ struct wrnn_handle {
         const float *wreg = nullptr, *wlds = nullptr;
         const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
         bool p1x4 = false;  // fatchord: P1 as [step][row][unit][r, z, n, cI] (one 16-B load)
+        const float *wwide = nullptr, *wwide_lds = nullptr;  // wide-row launches (MFMA images)
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
@@ -199,10 +200,24 @@ struct wrnn_handle {
     unsigned* prog_host = nullptr;  // host-mapped progress word (kernels publish steps done)
     unsigned* prog_dev = nullptr;
     int last_Bp = 0;                // rows the last call ran (padded to 8 * rows-per-group)
-    int p_nr = 0, p_nbatch = 0;     // PERSIST: rows per group per launch, row batches
+    struct PLaunch {
+        int rb, nr;  // first row, rows per XCD group (the launch runs rows rb + g + 8 r, r < nr)
+        bool wide;   // kernels_persist_wide.hip (MFMA) or the register-resident kernel
+    };
+    std::vector<PLaunch> p_plan;    // PERSIST: the launches of the last call, in order
+    std::vector<int> pev_kind;      // per timed launch: 1 wide, 0 otherwise
+    std::vector<int> pev_rows;      // per timed launch: rows (8 nr)
     std::vector<hipEvent_t> pev;    // PERSIST timing events (start, end) per launch
     std::vector<int> pev_steps;
     double p_step_bytes = 0, p_step_flops = 0;  // algorithmic per step
+    double p_wbytes = 0, p_row_bytes = 0, p_macs = 0;  // per step: weights, per row-step, MACs/row
+    struct PStage {
+        std::string name;  // "persist" (register-resident kernels) or "persist_wide"
+        int wide;
+        double rows;       // real rows summed over the kind's launches
+        int launches;
+    };
+    std::vector<PStage> pstages;  // launch kinds of the last PERSIST call
     double p_avg_steps = 0;                      // steps per timed launch
 
     ~wrnn_handle() {
@@ -416,6 +431,8 @@ int pack_p1(wrnn_handle* h, bool x4) {
     return WRNN_OK;
 }
 
+int pack_persist_wide(wrnn_handle* h);
+
 int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     auto& T = h->host;
     const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
@@ -475,6 +492,7 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     P.wlds = upload(h, wlds, &rc);
     CHECK(rc);
     CHECK(pack_p1(h, true));
+    CHECK(pack_persist_wide(h));
     auto dv = [&](const std::string& key) -> const float* {
         if (!h->dvec.count(key)) h->dvec[key] = upload(h, T[key], &rc);
         return h->dvec[key];
@@ -487,6 +505,58 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     P.oF1 = oF1;
     P.oF2 = oF2;
     P.ok = true;
+    return WRNN_OK;
+}
+
+// Wide-row launch weight images (kernels_persist_wide.hip): MFMA A operands. Slot w, wave v,
+// lane l, tile T, k-step ks: W_T[row 16 w + (l & 15)][unit 64 v + 16 (l >> 4) + ks]; registers
+// [w][v][40 float4 (4 T + ks / 4)][64 l] for T = W_ih2[:, :512] r, z, n | W_hh1 r, z, n | fc1 |
+// fc2 | fc3 (x parts only), LDS [w][3 T][v][4 q][64 l][4] for W_hh2 r, z, n.
+int pack_persist_wide(wrnn_handle* h) {
+    auto& T = h->host;
+    auto& P = h->pw;
+    P.wwide = P.wwide_lds = nullptr;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    if (h->cfg.mode != WRNN_MODE_RAW || n > kPM * 16 || H != kPH || F != kPH) return WRNN_OK;
+    const auto& Wih2 = T["rnn2.weight_ih_l0"];  // (3H, H + A)
+    const auto& Whh1 = T["rnn1.weight_hh_l0"];  // (3H, H)
+    const auto& Whh2 = T["rnn2.weight_hh_l0"];  // (3H, H)
+    const auto& Wf1 = T["fc1.weight"];          // (F, H + A)
+    const auto& Wf2 = T["fc2.weight"];          // (F, F + A)
+    const auto& Wf3 = T["fc3.weight"];          // (n, F)
+    auto elem = [&](int w, int t, int i, int k) -> float {
+        const int u = 16 * w + i;
+        switch (t) {
+            case 0: case 1: case 2: return Wih2[(size_t)(t * H + u) * (H + A) + k];
+            case 3: case 4: case 5: return Whh1[(size_t)((t - 3) * H + u) * H + k];
+            case 6: return Wf1[(size_t)u * (H + A) + k];
+            case 7: return Wf2[(size_t)u * (F + A) + k];
+            case 8: return u < n ? Wf3[(size_t)u * F + k] : 0.f;
+            default: return Whh2[(size_t)((t - 9) * H + u) * H + k];  // 9, 10, 11: r, z, n
+        }
+    };
+    std::vector<float> wr(persist_wide_wreg_floats()), wl(persist_wide_wlds_floats());
+    const int nq = (int)(wr.size() / ((size_t)kPM * 8 * 64 * 4));  // float4 per lane (40)
+    for (int w = 0; w < kPM; ++w)
+        for (int v = 0; v < 8; ++v)
+            for (int l = 0; l < 64; ++l) {
+                for (int q = 0; q < nq; ++q)
+                    for (int c = 0; c < 4; ++c) {
+                        const int t = q / 4, ks = 4 * (q % 4) + c;
+                        wr[((((size_t)w * 8 + v) * nq + q) * 64 + l) * 4 + c] =
+                            elem(w, t, l & 15, 64 * v + 16 * (l >> 4) + ks);
+                    }
+                for (int t = 0; t < 3; ++t)
+                    for (int q = 0; q < 4; ++q)
+                        for (int c = 0; c < 4; ++c)
+                            wl[(((((size_t)w * 3 + t) * 8 + v) * 4 + q) * 64 + l) * 4 + c] =
+                                elem(w, 9 + t, l & 15, 64 * v + 16 * (l >> 4) + 4 * q + c);
+            }
+    int rc = WRNN_OK;
+    P.wwide = upload(h, wr, &rc);
+    CHECK(rc);
+    P.wwide_lds = upload(h, wl, &rc);
+    CHECK(rc);
     return WRNN_OK;
 }
 
@@ -1404,8 +1474,8 @@ bool persist_device_ok(wrnn_handle* h) {
     hipDeviceProp_t p;
     bool ok = hipGetDeviceProperties(&p, d) == hipSuccess && p.multiProcessorCount == kPG * kPM &&
               std::strncmp(p.gcnArchName, "gfx950", 6) == 0 &&
-              p.sharedMemPerMultiprocessor >=
-                  std::max({persist_lds_bytes(), persist_rr_lds_bytes(), persist_gen_lds_bytes()});
+              p.sharedMemPerMultiprocessor >= std::max({persist_lds_bytes(), persist_rr_lds_bytes(),
+                                                        persist_gen_lds_bytes(), persist_wide_lds_bytes()});
     if (d >= 0 && d < 64) cached[d] = ok ? 1 : 2;
     return ok;
 }
@@ -1492,7 +1562,11 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
     CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
     const bool rr = W.rr, gen = W.gen;
-    const size_t xfl = gen ? persist_gen_xbuf_floats() : rr ? persist_rr_xbuf_floats() : persist_xbuf_floats();
+    bool any_wide = false;
+    for (const auto& L : h->p_plan) any_wide |= L.wide;
+    const size_t xfl = gen  ? persist_gen_xbuf_floats()
+                       : rr ? persist_rr_xbuf_floats()
+                            : std::max(persist_xbuf_floats(), any_wide ? persist_wide_xbuf_floats() : 0);
     CHECK(P.xbuf.alloc(xfl * sizeof(float)));
     CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? 11 * kRH : 6 * H) * sizeof(float)));
     // P1 (all steps, rows) was written by run_upsample next to cI; the noise by
@@ -1621,8 +1695,9 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     // batch, so the exchange area and flags are cleared before each. A progress callback does
     // not split launches: the kernels publish their step count to a host-mapped word every 100
     // steps (persist_common.h p_progress) and this thread reports from it while they run.
-    const int nb = h->p_nbatch;
-    a.nr = h->p_nr;
+    const int nb = (int)h->p_plan.size();
+    a.wwide = (const float4*)W.wwide;
+    a.wwide_lds = (const float4*)W.wwide_lds;
     if (cb && !h->prog_host) {
         HIPC(hipHostMalloc((void**)&h->prog_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
         HIPC(hipHostGetDevicePointer((void**)&h->prog_dev, h->prog_host, 0));
@@ -1632,10 +1707,14 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     for (auto e : h->pev) (void)hipEventDestroy(e);
     h->pev.clear();
     h->pev_steps.clear();
+    h->pev_kind.clear();
+    h->pev_rows.clear();
     if (h->timing) CHECK(P.stamps.alloc((size_t)nb * 2 * sizeof(uint32_t)));
     const auto t_start = std::chrono::steady_clock::now();
     for (int b = 0; b < nb; ++b) {
-        a.rb = b * kPG * a.nr;
+        const auto& L = h->p_plan[b];
+        a.rb = L.rb;
+        a.nr = L.nr;
         a.t0 = 0;
         a.t1 = S;
         a.prog_base = b * S;
@@ -1652,6 +1731,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             h->pev.push_back(e0);
             h->pev.push_back(e1);
             h->pev_steps.push_back(S);
+            h->pev_kind.push_back(L.wide ? 1 : 0);
+            h->pev_rows.push_back(kPG * L.nr);
             HIPC(hipEventRecord(e0, st));
         }
         if (gen) {
@@ -1670,6 +1751,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.stamps = a.stamps;
             ar.prog_base = a.prog_base;
             HIPC(launch_persist_rr(ar, st));
+        } else if (L.wide) {
+            HIPC(launch_persist_wide(a, st));
         } else {
             HIPC(launch_persist(a, st));
         }
@@ -1728,10 +1811,23 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         wparams += (double)kv.second.size();
         if (k.find("weight") != std::string::npos) macs += (double)kv.second.size();
     }
-    // per launch: one row batch (real rows averaged over the batches)
-    const double rows_l = (double)B / nb;
-    h->p_step_bytes = 4.0 * wparams + rows_l * ((h->feat + h->R) * 4.0 + 2.0);
-    h->p_step_flops = 2.0 * macs * rows_l;
+    // per launch kind (register-resident / wide): real rows averaged over its launches
+    h->p_wbytes = 4.0 * wparams;
+    h->p_row_bytes = (h->feat + h->R) * 4.0 + 2.0;
+    h->p_macs = macs;
+    h->pstages.clear();
+    for (const auto& L : h->p_plan) {
+        const int real = std::max(0, std::min(B, L.rb + kPG * L.nr) - L.rb);
+        const char* nm = L.wide ? "persist_wide" : "persist";
+        auto it = std::find_if(h->pstages.begin(), h->pstages.end(),
+                               [&](const wrnn_handle::PStage& q) { return q.name == nm; });
+        if (it == h->pstages.end()) {
+            h->pstages.push_back({nm, L.wide ? 1 : 0, 0.0, 0});
+            it = h->pstages.end() - 1;
+        }
+        it->rows += real;
+        it->launches += 1;
+    }
     return WRNN_OK;
 }
 
@@ -1777,47 +1873,80 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         else if (!std::strcmp(env, "auto")) want = WRNN_ENGINE_AUTO;
     }
     std::string why;
-    // PERSIST row batches: the largest register-resident rows-per-group variant bounds one
-    // launch at 8 * nr_max rows; more rows run as consecutive launches over row batches, with
-    // the rows spread evenly over the batches (nr rows per group each)
-    int nr_max = 0;
-    if (h->pw.ok)
-        for (int r = kPNR; r >= 1 && !nr_max; --r)
-            if (h->pw.gen  ? persist_gen_variant_ok(r, h->pw.cpw)
-                : h->pw.rr ? persist_rr_variant_ok(r, h->pw.cpw)
-                           : persist_variant_ok(r, h->pw.cpw))
-                nr_max = r;
-    // fatchord: rows per group by launch cost. A launch with more rows per group runs each
-    // step slower (measured MI355X us per step below; the larger variants may also hold a few
-    // spilled registers), so more rows per launch pay only when they save launches:
-    // 9-bit 30 rows -> one launch at 4 rows, 144 rows -> six at 3; 10-bit 45 rows -> two at 3.
-    if (h->pw.ok && !h->pw.gen && !h->pw.rr) {
-        static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
-        const int wide = h->pw.cpw > 16 ? 1 : 0;
-        double best = 0;
-        nr_max = 0;
-        for (int c = 1; c <= kPNR; ++c) {
-            const int sc = persist_variant_scratch(c, h->pw.cpw);
-            if (sc < 0 || sc > 64) continue;
-            const int nb = (B + kPG * c - 1) / (kPG * c), n = (B + kPG * nb - 1) / (kPG * nb);
-            const double cost = nb * us[wide][n];
-            if (!nr_max || cost <= best) {
-                nr_max = c;
-                best = cost;
+    // PERSIST launch plan: consecutive launches over row batches; launch k runs rows
+    // rb_k + g + 8 r (r < nr_k) in every XCD group g. Candidate launches per topology:
+    //  * register-resident kernels (kernels_persist*.hip) with nr rows per group, nr up to the
+    //    largest variant without register spills;
+    //  * fatchord RAW <= 512 classes: the wide MFMA kernel (kernels_persist_wide.hip), up to
+    //    16 rows per group.
+    // The plan minimises the summed per-step time of its launches (measured MI355X us per step
+    // below), e.g. 9-bit: 18 rows -> one launch at 3 rows; 144 rows -> one wide launch of 128
+    // rows + one launch at 2 rows.
+    std::vector<wrnn_handle::PLaunch> lplan;
+    if (h->pw.ok) {
+        struct Opt {
+            int nr;
+            bool wide;
+            double us;
+        };
+        std::vector<Opt> opts;
+        if (!h->pw.gen && !h->pw.rr) {
+            static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
+            const int w10 = h->pw.cpw > 16 ? 1 : 0;
+            for (int c = 1; c <= kPNR; ++c) {
+                const int sc = persist_variant_scratch(c, h->pw.cpw);
+                if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[w10][c]});
+            }
+            int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
+            if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
+            if (wmode && h->pw.wwide && persist_wide_scratch() == 0) {
+                if (wmode == 1) opts.clear();
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 8.0 + 0.12 * r});
+            }
+        } else {
+            for (int r = kPNR; r >= 1; --r)
+                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw) : persist_rr_variant_ok(r, h->pw.cpw)) {
+                    opts.push_back({r, false, 1.0});  // one launch per batch of the largest variant
+                    break;
+                }
+        }
+        if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B
+            const int c = std::max(1, std::min(kPNR, std::atoi(env)));
+            opts.erase(std::remove_if(opts.begin(), opts.end(), [&](const Opt& o) { return o.wide || o.nr != c; }),
+                       opts.end());
+            if (opts.empty()) opts.push_back({c, false, 1.0});
+        }
+        if (!opts.empty()) {
+            // best[r]: cheapest plan for r rows; pick[r]: its first launch
+            std::vector<double> best(B + 1, 0.0);
+            std::vector<int> pick(B + 1, -1);
+            for (int r = 1; r <= B; ++r) {
+                best[r] = 1e300;
+                for (int o = 0; o < (int)opts.size(); ++o) {
+                    const double c = opts[o].us + best[std::max(0, r - kPG * opts[o].nr)];
+                    if (c < best[r] - 1e-9) {
+                        best[r] = c;
+                        pick[r] = o;
+                    }
+                }
+            }
+            int rb = 0;
+            for (int r = B; r > 0;) {
+                const Opt& o = opts[pick[r]];
+                lplan.push_back({rb, o.nr, o.wide});
+                rb += kPG * o.nr;
+                r = std::max(0, r - kPG * o.nr);
             }
         }
     }
-    if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX"))  // diagnostic: variant A/B
-        if (h->pw.ok) nr_max = std::max(1, std::min(kPNR, std::atoi(env)));
-    const int nbatch = nr_max ? (B + kPG * nr_max - 1) / (kPG * nr_max) : 0;
-    const int nr = nbatch ? (B + kPG * nbatch - 1) / (kPG * nbatch) : 0;
+    const int Bplan = lplan.empty() ? B : lplan.back().rb + kPG * lplan.back().nr;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
         if (!h->pw.ok)
             why = "model is not fatchord (512 / 512), runtimeracer (256 / 256) or geneing (256 / 128) "
                   "with <= 1024 classes";
-        else if (!nr_max) why = "no register-resident variant for this class count";
-        else if ((double)S * kPG * nr * nbatch * (4 * h->H + h->n_classes) * 4.0 > kPersistWsBytes)
+        else if (lplan.empty()) why = "no register-resident variant for this class count";
+        else if ((double)S * Bplan * (4 * h->H + h->n_classes) * 4.0 > kPersistWsBytes)
             why = "P1 / noise workspace for " + std::to_string(B) + " rows x " + std::to_string(S) +
                   " steps exceeds " + std::to_string((long long)(kPersistWsBytes / (1 << 30))) + " GiB";
         else if (h->persist_failed && want != WRNN_ENGINE_PERSIST)
@@ -1829,9 +1958,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         if (want == WRNN_ENGINE_PERSIST && !use_p)
             return fail(WRNN_ERR_INVALID, "persist engine unavailable: " + why);
     }
-    const int Bp = use_p ? kPG * nr * nbatch : B;  // persistent groups carry nr rows per batch
-    h->p_nr = use_p ? nr : 0;
-    h->p_nbatch = use_p ? nbatch : 0;
+    const int Bp = use_p ? Bplan : B;  // persistent groups carry nr rows per launch
+    h->p_plan = use_p ? lplan : std::vector<wrnn_handle::PLaunch>();
     CHECK(ensure_workspace(h, Bp, S, P, Fr, Tmax));
     auto& ws = h->ws;
     h->last_B = B;
@@ -1919,22 +2047,27 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
 
 int collect_timing(wrnn_handle* h) {
     if (h->last_engine == WRNN_ENGINE_PERSIST) {
-        // one stage: HIP-event duration of each persistent launch on its own stream
-        h->stage_avg_us.assign(1, 0.0);
-        h->stage_launches.assign(1, 0);
+        // one stage per launch kind: HIP-event duration of each persistent launch on its stream
+        const int ns = (int)h->pstages.size();
+        h->stage_avg_us.assign(ns, 0.0);
+        h->stage_launches.assign(ns, 0);
         h->p_avg_steps = 0;
         if (!h->timing || h->pev.empty()) return WRNN_OK;
         HIPC(hipStreamSynchronize(h->stream));
-        double tot = 0, steps = 0;
+        double steps = 0;
         const int nl = (int)h->pev.size() / 2;
         for (int i = 0; i < nl; ++i) {
             float ms = 0;
             HIPC(hipEventElapsedTime(&ms, h->pev[2 * i], h->pev[2 * i + 1]));
-            tot += ms * 1000.0;
+            for (int k = 0; k < ns; ++k)
+                if (h->pstages[k].wide == h->pev_kind[i]) {
+                    h->stage_avg_us[k] += ms * 1000.0;
+                    h->stage_launches[k] += 1;
+                }
             steps += h->pev_steps[i];
         }
-        h->stage_avg_us[0] = tot / nl;
-        h->stage_launches[0] = nl;
+        for (int k = 0; k < ns; ++k)
+            if (h->stage_launches[k]) h->stage_avg_us[k] /= h->stage_launches[k];
         h->p_avg_steps = steps / nl;
         return WRNN_OK;
     }
@@ -2219,13 +2352,17 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
                     double* flops, int* n_stages) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
     if (h->last_engine == WRNN_ENGINE_PERSIST) {
-        if (n_stages) *n_stages = 1;
-        if (stage != 0) return fail(WRNN_ERR_INVALID, "bad stage index");
-        if (name && name_cap) std::snprintf(name, name_cap, "%s", "persist");
-        // per launch = steps per launch x per-step algorithmic bytes / FLOPs
+        const int ns = (int)h->pstages.size();
+        if (n_stages) *n_stages = ns;
+        if (stage < 0 || stage >= ns) return fail(WRNN_ERR_INVALID, "bad stage index");
+        const auto& q = h->pstages[stage];
+        if (name && name_cap) std::snprintf(name, name_cap, "%s", q.name.c_str());
+        // per launch = steps x (recurrent weights once per step + the launch's real rows x
+        // per-row-step stream) / FLOPs
         const double steps = h->p_avg_steps > 0 ? h->p_avg_steps : h->last_S;
-        if (bytes) *bytes = steps * h->p_step_bytes;
-        if (flops) *flops = steps * h->p_step_flops;
+        const double rows = q.launches ? q.rows / q.launches : 0.0;
+        if (bytes) *bytes = steps * (h->p_wbytes + rows * h->p_row_bytes);
+        if (flops) *flops = steps * 2.0 * h->p_macs * rows;
         return WRNN_OK;
     }
     if (n_stages) *n_stages = (int)h->stages.size();

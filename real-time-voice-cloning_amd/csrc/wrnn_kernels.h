@@ -203,9 +203,21 @@ struct PersistArgs {
     int phase_t;
     unsigned* progress;     // optional host-mapped word: steps done (persist_common.h p_progress)
     int prog_base;          // row batch * S
+    // wide-row launches (kernels_persist_wide.hip): MFMA A-operand weight images
+    const float4* wwide;    // [kPM][8 waves][40 float4][64 lanes]
+    const float4* wwide_lds;// [kPM][2 tiles][8][4][64] (W_hh2 z, n)
 };
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
+// Wide-row fatchord launch: up to kPWideRows rows per XCD group (8 kPWideRows per launch),
+// fp32 MFMA products, RAW categorical with <= 512 classes.
+constexpr int kPWideRows = 16;
+hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
+size_t persist_wide_lds_bytes();
+size_t persist_wide_xbuf_floats();
+size_t persist_wide_wreg_floats();
+size_t persist_wide_wlds_floats();
+int persist_wide_scratch();
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
 // ---------------------------------------------------------------------------------------

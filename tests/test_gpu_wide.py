@@ -1,0 +1,93 @@
+"""The wide-row persistent launch (kernels_persist_wide.hip: 16 rows per XCD group, fp32 MFMA
+products, distributed GRU1, five hops per step) against the reference's golden outputs and the
+oracle. ``WRNN_PERSIST_WIDE=1`` makes every launch of a call wide (1..16 rows per group);
+the default plan mixes wide and register-resident launches by cost (C4: 128 + 16 rows).
+
+Reference step: vocoder/models/fatchord_version.py:192-236; bar: bit-exact 9-bit labels.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def wide_only():
+    old = os.environ.get('WRNN_PERSIST_WIDE')
+    os.environ['WRNN_PERSIST_WIDE'] = '1'
+    yield
+    if old is None:
+        del os.environ['WRNN_PERSIST_WIDE']
+    else:
+        os.environ['WRNN_PERSIST_WIDE'] = old
+
+
+def _stage_names(m):
+    return [s[0] for s in m.stage_info()]
+
+
+@pytest.mark.parametrize('name', ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny',
+                                  'fatchord_raw9_config1'])
+def test_wide_golden_bit_exact(name, wide_only):
+    meta, gold = golden_case(name)
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    m, hp, sd = make_model(meta)
+    m.set_engine('persist')
+    m.enable_stage_timing(True)
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    wav = m.generate(mel[None], meta['batched'], meta['target'], meta['overlap'], hp.mu_law,
+                     sp.preemphasize, progress_callback=lambda *a: None)
+    assert _stage_names(m) == ['persist_wide']
+    assert np.array_equal(m.last_labels, gold['labels'])
+    assert np.array_equal(wav, gold['wav'])
+
+
+@pytest.mark.parametrize('n_utts', [3, 13, 26])
+def test_wide_row_counts_match_oracle(n_utts, wide_only):
+    """5 fold rows per utterance -> 15 / 65 / 130 rows: 2, 9 and 16 + 1 rows per group (the
+    last over two wide launches), every row against the oracle."""
+    import torch
+    from oracle.wavernn_oracle import oracle_infer_waveform
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_raw9_tiny')
+    m, hp, sd = make_model(meta)
+    mels = [synth_mel(meta['n_frames'], 400 + u) / sp.max_abs_value for u in range(n_utts)]
+    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
+    m.set_engine('persist')
+    m.set_seed(meta['noise_seed'])
+    m.enable_stage_timing(True)
+    lab, roff, S = m.generate_batch_device(dev, True, meta['target'], meta['overlap'])
+    assert _stage_names(m) == ['persist_wide']
+    lab = lab.cpu().numpy()
+    for u in sorted({0, n_utts // 2, n_utts - 1}):
+        ref = oracle_infer_waveform(sd, hp, meta['model_type'], mels[u] * sp.max_abs_value,
+                                    target=meta['target'], overlap=meta['overlap'],
+                                    seed=meta['noise_seed'], stream=u)
+        got = lab[roff[u]:roff[u + 1]]
+        d = np.argwhere(got != ref['labels'])
+        assert len(d) == 0, f'utt {u}: first divergence {d[np.argmin(d[:, 1])] if len(d) else None}'
+
+
+def test_default_plan_uses_wide_launch_for_c4_rows():
+    """144 rows (C4 per GPU) -> one wide launch of 128 rows + one register-resident launch."""
+    import torch
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_raw9_tiny')
+    m, hp, sd = make_model(meta)
+    mels = [torch.from_numpy((synth_mel(1000, u) / sp.max_abs_value).astype(np.float32)).cuda()
+            for u in range(8)]
+    m.enable_stage_timing(True)
+    out, roff, S = m.generate_batch_device(mels, True, 11000, 550)
+    assert roff[-1] == 144
+    names = _stage_names(m)
+    assert 'persist_wide' in names, names
