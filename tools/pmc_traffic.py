@@ -16,20 +16,27 @@ REPO = os.path.dirname(HERE)
 CORR = ('FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE reports half the '
         'bytes of wide coalesced reads; this kernel\'s streamed reads are 4 B/lane dword loads, a '
         'width the guide lists as uncalibrated); WRITE_SIZE as reported')
-# bench.py arguments of each measured topology (tools/measure.sh ARGS)
-MODELS = {'fat': ('fatchord-wavernn', 'RAW', 9, ''),
-          'rr': ('runtimeracer-wavernn', 'RAW', 9, ' --model runtimeracer-wavernn --bits 9'),
-          'gen': ('geneing-wavernn', 'BITS', 10, ' --model geneing-wavernn --mode BITS --bits 10')}
-
-
-def workload(model, mode, bits, frames=1000, utts=1, target=11000, overlap=550):
-    return (f'{utts}x{frames}-frame mel per GPU, {model} {mode} {bits}-bit mu-law, '
+# workload -> (bench.py arguments as in tools/measure.sh ARGS, bench workload string, kernel key)
+def workload(model, wname, frames=1000, utts=1, target=11000, overlap=550):
+    return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
             f'batched folds target={target} overlap={overlap}')
 
 
-def counter(path):
-    rows = [r for r in csv.DictReader(open(path)) if 'k_persist' in r['Kernel_Name']
-            and '_init' not in r['Kernel_Name']]
+WORKLOADS = {
+    'c2': ('', workload('fatchord-wavernn', 'RAW 9-bit mu-law'), 'k_persist'),
+    'c4': (' --utts-per-gpu 8', workload('fatchord-wavernn', 'RAW 9-bit mu-law', utts=8), 'k_persist_wide'),
+    'c3': (' --mode MOL', workload('fatchord-wavernn', 'MOL'), 'k_persist'),
+    'rr': (' --model runtimeracer-wavernn --bits 9', workload('runtimeracer-wavernn', 'RAW 9-bit mu-law'),
+           'k_persist'),
+    'gen': (' --model geneing-wavernn --mode BITS --bits 10', workload('geneing-wavernn', 'BITS 10-bit'),
+            'k_persist'),
+}
+
+
+def counter(path, kernel):
+    def base(name):  # 'void wrnn::k_persist<3, false>(wrnn::PersistArgs)' -> 'k_persist'
+        return name.split('(')[0].split('<')[0].split('::')[-1]
+    rows = [r for r in csv.DictReader(open(path)) if base(r['Kernel_Name']) == kernel]
     return rows[0]['Kernel_Name'], sum(float(r['Counter_Value']) for r in rows), len(rows)
 
 
@@ -38,24 +45,24 @@ def main():
     os.makedirs(os.path.join(out, 'pmc'), exist_ok=True)
     jpath = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     table = json.load(open(jpath)) if os.path.exists(jpath) else {}
-    for key, (model, mode, bits, extra) in MODELS.items():
+    for key, (extra, wl, kernel) in WORKLOADS.items():
         f = os.path.join(src, f'pmc_fetch_{key}', 'run_counter_collection.csv')
         w = os.path.join(src, f'pmc_write_{key}', 'run_counter_collection.csv')
         if not (os.path.exists(f) and os.path.exists(w)):
             continue
-        kname, fetch, n = counter(f)
-        _, write, _ = counter(w)
+        kname, fetch, n = counter(f, kernel)
+        _, write, _ = counter(w, kernel)
         dst_f = os.path.join(out, 'pmc', f'fetch_size_{key}.csv')
         dst_w = os.path.join(out, 'pmc', f'write_size_{key}.csv')
         shutil.copy(f, dst_f)
         shutil.copy(w, dst_w)
         traffic = (2 * fetch + write) * 1024.0 / n  # KiB counters, per launch
-        table[f'k_persist|{workload(model, mode, bits)}'] = {
+        table[f'{kernel}|{wl}'] = {
             'kernel': kname, 'launches': n, 'fetch_size_kib': fetch / n, 'write_size_kib': write / n,
             'traffic_bytes': traffic, 'correction': CORR,
             'source': f'{os.path.relpath(dst_f, REPO)}, {os.path.relpath(dst_w, REPO)}: rocprofv3 '
                       f'--pmc FETCH_SIZE | WRITE_SIZE (separate passes) --kernel-include-regex '
-                      f'k_persist -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 '
+                      f'{kernel} -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 '
                       f'--no-timing{extra}'}
         print(key, kname, f'{traffic / 1e9:.3f} GB per launch')
     json.dump(table, open(jpath, 'w'), indent=1)
