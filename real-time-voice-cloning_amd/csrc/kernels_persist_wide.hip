@@ -44,10 +44,7 @@ constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
 constexpr int WL_GH1 = 0;                        // gh1 of the slot's units [3][16 n][16 ul]
 constexpr int WL_GH2 = WL_GH1 + 768;             // gh2 [3][16 n][16 ul]
 constexpr int WL_X1 = WL_GH2 + 768;              // x1 of the slot's units [16 n][16 ul]
-constexpr int WL_SX = WL_X1 + 256;               // sample per row [16]
-constexpr int WL_CV = WL_SX + 16;                // hop-D partial argmax [4][16] value, class
-constexpr int WL_CI = WL_CV + 64;
-constexpr int WL_RI = WL_CI + 64;                // RowInfo of the group's rows (6 words each)
+constexpr int WL_RI = WL_X1 + 256;               // RowInfo of the group's rows (6 words each)
 constexpr int WL_FAIL = WL_RI + 16 * 6;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
@@ -299,6 +296,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 y = y > 0.f ? y : 0.f;
             }
             pub(WB_Y1, y, seq);
+        } else {  // gh1 = sum of the W_hh1 h1 partials + b_hh1 (waves 4-7; read by GRU1)
+            const int i = tid - 256, rn = i >> 4, ul = i & 15;
+            if (rn < R)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
+                    lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
+                        p_add(s, bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                }
         }
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
@@ -375,108 +383,75 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         wbar();
         WSTAMP(9);
         if (lds[WL_FAIL] != 0.f) return;
-        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
         if (lo) {
+            const unsigned tag_hi = (seq & kTagSeqMask) << 11;
             // fc3 epilogue: candidate argmax_k (l_k + g_k) over the slot's 16 classes per row
             // (row cn = one DPP row of 16 lanes), published tagged by lane cul == 0
-            float val = -INFINITY;
-            int cls = cu;
-            if (cell && cu < a.n_classes) {
-                float s = 0.f;
-#pragma unroll
-                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
-                val = p_add(p_add(s, bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)), pg);
-            }
-            row16_argmax(val, cls);
-            if (cell && cul == 0)
-                __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls}, xr,
-                                                      (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
-        } else {  // gh1 = sum of the W_hh1 h1 partials + b_hh1 (waves 4-7)
-            const int i = tid - 256, rn = i >> 4, ul = i & 15;
-            if (rn < R)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
+            {
+                float val = -INFINITY;
+                int cls = cu;
+                if (cell && cu < a.n_classes) {
                     float s = 0.f;
 #pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
-                    lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
+                    val = p_add(p_add(s, bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)), pg);
                 }
-        }
-        // ================= hop D: sample of step t (wave 0, every workgroup) ===============
-        if (v == 0) {
-            const int n = l & 15, gq = l >> 4;  // row n, slots 8 gq .. 8 gq + 7
-            const bool valid = n < R;
-            const unsigned off = (unsigned)((n * 32 + 8 * gq) * 2) * 4u;
-            const unsigned want = seq & kTagSeqMask;
-            u4v q[4] = {(u4v){0u, want << 11, 0u, want << 11}, (u4v){0u, want << 11, 0u, want << 11},
-                        (u4v){0u, want << 11, 0u, want << 11}, (u4v){0u, want << 11, 0u, want << 11}};
-            const unsigned t0s = p_now();
-            unsigned nsp = 0;
-            while (true) {
-                bool ok = true;
-                if (valid) {
-                    unsigned vo = off;
-                    asm volatile("" : "+v"(vo));
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        q[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, WX_D * 4 + 16u * k, kCpNT);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) ok = ok && (q[k].y >> 11) == want && (q[k].w >> 11) == want;
-                }
-                if (__all(ok)) break;
-                if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
-                    if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
-                    fail = true;
-                    break;
-                }
+                row16_argmax(val, cls);
+                if (cell && cul == 0)
+                    __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls},
+                                                          xr, (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
             }
-            float bv = -INFINITY;
-            int bi = 0x7fffffff;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // slots in ascending order; ties -> lowest class
-                const float v0 = __uint_as_float(q[k].x), v1 = __uint_as_float(q[k].z);
-                const int k0 = (int)(q[k].y & 0x7ffu), k1 = (int)(q[k].w & 0x7ffu);
-                if (v0 > bv || (v0 == bv && k0 < bi)) { bv = v0; bi = k0; }
-                if (v1 > bv || (v1 == bv && k1 < bi)) { bv = v1; bi = k1; }
-            }
-            lds[WL_CV + gq * 16 + n] = bv;
-            lds[WL_CI + gq * 16 + n] = __int_as_float(bi);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (gq == 0 && valid) {
-#pragma unroll
-                for (int k = 1; k < 4; ++k) {
-                    const float v2 = lds[WL_CV + k * 16 + n];
-                    const int k2 = __float_as_int(lds[WL_CI + k * 16 + n]);
-                    if (v2 > bv || (v2 == bv && k2 < bi)) { bv = v2; bi = k2; }
+            // ============= hop D: sample of step t, per cell wave for its own 4 rows ========
+            // lane (row cn, cul) reads the candidates of slots 2 cul, 2 cul + 1 of its row; the
+            // row's 16 lanes reduce them (DPP), so every cell of the row holds the sample
+            float x;
+            {
+                const unsigned want = seq & kTagSeqMask;
+                u4v q = {0u, want << 11, 0u, want << 11};
+                const unsigned t0s = p_now();
+                unsigned nsp = 0;
+                while (true) {
+                    if (cell) {
+                        unsigned vo = (unsigned)((cn * 32 + 2 * cul) * 2) * 4u;
+                        asm volatile("" : "+v"(vo));
+                        q = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, WX_D * 4, kCpNT);
+                    }
+                    if (__all((q.y >> 11) == want && (q.w >> 11) == want)) break;
+                    if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
+                        if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                        fail = true;
+                        break;
+                    }
                 }
-                float xv;
+                float bv = __uint_as_float(q.x);
+                int bi = (int)(q.y & 0x7ffu);
+                const float v1 = __uint_as_float(q.z);
+                const int k1 = (int)(q.w & 0x7ffu);
+                if (v1 > bv || (v1 == bv && k1 < bi)) {  // ties -> lowest class
+                    bv = v1;
+                    bi = k1;
+                }
+                row16_argmax(bv, bi);
                 {
 #pragma clang fp contract(off)
-                    xv = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
+                    x = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
                 }
-                lds[WL_SX + n] = xv;
-                if (w == 0) {
-                    int nn = n;
+                if (w == 0 && cell && cul == 0) {
+                    int nn = cn;
                     asm volatile("" : "+v"(nn));
                     const unsigned ro = (unsigned)((g0 + kPG * nn) * a.ld);
                     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels), ro * 2u,
                                                           (unsigned)t * 2u, 0);
-                    bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                    bst(x, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
                 }
             }
-        }
-        if (fail) lds[WL_FAIL] = 1.f;
-        wbar();
-        WSTAMP(10);
-        if (lds[WL_FAIL] != 0.f) return;
-        // ================= GRU1 of step t + 1 for the slot's units -> publish x1, h1 ========
-        //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
-        // (at the last step it runs on clamped inputs and nobody reads the result)
-        if (lo) {
+            if (fail) lds[WL_FAIL] = 1.f;  // seen by every wave after the next barrier
+            WSTAMP(10);
+            // ============= GRU1 of step t + 1 for the slot's units -> publish x1, h1 ========
+            //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
+            // (at the last step it runs on clamped inputs and nobody reads the result)
             float x1 = 0.f;
             if (cell) {
-                const float x = lds[WL_SX + cn];
                 const float* gh = lds + WL_GH1 + cn * 16 + cul;
                 h1r = p_gru(fmaf(vj0, x, pp.x), fmaf(vj1, x, pp.y), fmaf(vj2, x, pp.z), gh[0], gh[256],
                             gh[512], h1r);

@@ -1899,11 +1899,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             }
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
             if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
-            if (wmode && h->pw.wwide && persist_wide_scratch() == 0) {
+            // (a variant with register spills is not used unless WRNN_WIDE_ALLOW_SCRATCH=1: A/B)
+            const bool scratch_ok = persist_wide_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
+            if (wmode && h->pw.wwide && scratch_ok) {
                 if (wmode == 1) opts.clear();
-                // measured: 13.2 us per step at 16 rows per group (the MFMA tiles cost the same
+                // measured: 12.3 us per step at 16 rows per group (the MFMA tiles cost the same
                 // for any row count; the exchanges shrink a little with fewer rows)
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 12.0 + 0.08 * r});
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 11.1 + 0.08 * r});
             }
         } else {
             for (int r = kPNR; r >= 1; --r)
