@@ -55,6 +55,8 @@ extern "C" {
 
 #define WRNN_MODE_RAW 0 /* softmax over 2**bits classes, Categorical sample (geneing: 'BITS') */
 #define WRNN_MODE_MOL 1 /* 10-component discretized mixture of logistics   */
+#define WRNN_MODE_BETA 2 /* geneing 'RAW': Beta(exp(l0), exp(l1)) on 2 outputs
+                            (geneing_version.py:95-96,207-210, distribution.py:7-20) */
 
 /* Recurrence engines (same results, different schedules):
  *   CHAIN   one launch per layer group per step, HIP-graph captured (every topology)
@@ -196,6 +198,11 @@ int wrnn_post_overlaps(const int16_t* labels, int nf, int S, int overlap, const 
 int wrnn_post_assemble(const int16_t* labels, int nf, int S, int overlap, const double* mid_lut,
                        int n_classes, const double* regions, int preemph, double coef,
                        const double* fade, size_t fade_len, double* out, size_t n_out);
+
+/* Host restatement of the BETA noise contract (no device): the sample of one (step, row)
+ * for Beta(alpha, beta), rescaled to [-1, 1] -- the value the kernels compute (tests). */
+int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,
+                    float beta, float* out);
 
 /* Raw access for tests: copy the RAW noise (seq_len, rows, n_classes) of the last call's
  * first `n_steps` steps to host (float32). */

@@ -30,6 +30,16 @@ MOL  : counter = (0x80000000 | j, step, row, stream) for j = 0, 1, 2 -> 12 words
        U = (w >> 8) * 2**-24
        u = float32(1e-5 + (1 - 1e-5 - 1e-5) * U)  (torch ``uniform_(1e-5, 1.0 - 1e-5)``)
        u1[m] = u(w[m]) for the 10 mixtures, u2 = u(w[10])
+BETA : geneing 'RAW' mode, ``vocoder/distribution.py:7-20`` ``Beta(alpha, beta).sample()``
+       (torch: Dirichlet over two standard gammas, rejection-sampled from the global generator)
+       restated on the stream as X / (X + Y), X ~ Gamma(alpha), Y ~ Gamma(beta) by
+       Marsaglia-Tsang (2000) in float64, gamma g = 0 (alpha) / 1 (beta), attempt k < 16:
+       counter = (0x40000000 | g << 8 | k, step, row, stream) -> 4 words, u_i as RAW's u
+       (open (0, 1)); a' = a + 1 if a < 1 else a; d = a' - 1/3; c = 1 / sqrt(9 d)
+       z = sqrt(-2 log u0) * cos(2 pi u1); t = 1 + c z; v = (t t) t
+       accept the first k with v > 0 and log u2 < ((0.5 z) z + d - d v) + d log v: G = d v
+       (no accepted attempt: G = d); a < 1: G = G * u3 ** (1 / a) (u3 of the accepted attempt)
+       G = max(G, DBL_MIN); sample = float32(X / (X + Y)); returned 2 sample - 1 in float32
 """
 import numpy as np
 
@@ -42,6 +52,8 @@ MASK32 = np.uint64(0xFFFFFFFF)
 MOL_DOMAIN = 0x80000000
 MOL_LO = 1e-5
 MOL_HI = 1.0 - 1e-5
+BETA_DOMAIN = 0x40000000
+BETA_TRIES = 16
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
@@ -112,3 +124,48 @@ def mol_uniforms(seed, stream, steps, rows):
     U = (w >> np.uint32(8)).astype(np.float64) * (2.0 ** -24)
     u = (MOL_LO + (MOL_HI - MOL_LO) * U).astype(np.float32)
     return u[..., :10].copy(), u[..., 10].copy()
+
+
+def _u_open(x):
+    """Open-interval uniform of a 32-bit word, as RAW's (2 (x >> 9) + 1) 2**-24, float64."""
+    return (2.0 * (np.asarray(x, dtype=np.uint32) >> np.uint32(9)).astype(np.float64) + 1.0) * (2.0 ** -24)
+
+
+def gamma_mt(seed, stream, step, rows, a, g):
+    """Standard gamma variates (float64, shape (B,)) of shape a (float64 (B,)) for gamma index g
+    (0 alpha, 1 beta) at one step -- Marsaglia-Tsang on the Philox stream (BETA contract)."""
+    k0, k1 = seed_key(seed)
+    rows = np.asarray(rows, dtype=np.uint32)
+    a = np.asarray(a, dtype=np.float64)
+    boost = a < 1.0
+    ap = np.where(boost, a + 1.0, a)
+    d = ap - 1.0 / 3.0
+    c = 1.0 / np.sqrt(9.0 * d)
+    out = d.copy()
+    ub = np.ones_like(a)
+    done = np.zeros(a.shape, dtype=bool)
+    with np.errstate(invalid='ignore', divide='ignore'):
+        for k in range(BETA_TRIES):
+            w = philox4x32_10(np.uint32(BETA_DOMAIN | (g << 8) | k), np.uint32(step), rows,
+                              np.uint32(stream), k0, k1)
+            u0, u1, u2, u3 = (_u_open(x) for x in w)
+            z = np.sqrt(-2.0 * np.log(u0)) * np.cos(2.0 * np.pi * u1)
+            t = 1.0 + c * z
+            v = (t * t) * t
+            vpos = v > 0.0
+            rhs = ((0.5 * z) * z + d - d * v) + d * np.log(np.where(vpos, v, 1.0))
+            take = vpos & (np.log(u2) < rhs) & ~done
+            out = np.where(take, d * v, out)
+            ub = np.where(take, u3, ub)
+            done |= take
+    out = np.where(boost, out * np.power(ub, 1.0 / a), out)
+    return np.maximum(out, np.finfo(np.float64).tiny)
+
+
+def beta_sample(seed, stream, step, rows, alpha, beta):
+    """Beta(alpha, beta) rescaled to [-1, 1] (float32, shape (B,)) -- the BETA contract.
+    alpha, beta: float32 arrays (exp of the two fc3 outputs, vocoder/distribution.py:14-16)."""
+    x = gamma_mt(seed, stream, step, rows, np.asarray(alpha, np.float32).astype(np.float64), 0)
+    y = gamma_mt(seed, stream, step, rows, np.asarray(beta, np.float32).astype(np.float64), 1)
+    s = (x / (x + y)).astype(np.float32)
+    return np.float32(2.0) * s - np.float32(1.0)

@@ -10,7 +10,8 @@ What it restates (same torch ops, same order, same fp32/f64 dtypes as the refere
 * ``WaveRNN.generate``          vocoder/models/fatchord_version.py:155-259
                                 vocoder/models/runtimeracer_version.py:199-314
                                 vocoder/models/geneing_version.py:157-253 (I, rnn1, fc1, fc3;
-                                2-way aux split; BITS = categorical over 2**bits, no mu-law)
+                                2-way aux split; BITS = categorical over 2**bits, no mu-law;
+                                RAW = Beta(exp(l0), exp(l1)) on the Philox BETA contract)
 * ``UpsampleNetwork.forward``   fatchord_version.py:78-85 (+ MelResNet :38-44, ResBlock :17-24,
                                 Stretch2d :53-57); runtimeracer_version.py:88-95
 * ``pad_tensor``                fatchord_version.py:275-288
@@ -60,9 +61,9 @@ class OracleWaveRNN:
         self.model_type = model_type
         self.mode = hp.mode
         self.pad = hp.pad
-        if model_type == MODEL_TYPE_GENEING and hp.mode == 'RAW':
-            raise NotImplementedError('geneing RAW mode (Beta sampling) has no noise contract')
-        self.n_classes = 2 ** hp.bits if hp.mode in ('RAW', 'BITS') else 30
+        # geneing_version.py:95-101: 'RAW' = the 2 parameters of a Beta distribution
+        self.beta = model_type == MODEL_TYPE_GENEING and hp.mode == 'RAW'
+        self.n_classes = 2 if self.beta else 2 ** hp.bits if hp.mode in ('RAW', 'BITS') else 30
         self.rnn_dims = hp.rnn_dims
         # geneing_version.py:106 splits the aux into 2 parts, the others into 4
         self.n_aux = 2 if model_type == MODEL_TYPE_GENEING else 4
@@ -297,7 +298,15 @@ class OracleWaveRNN:
                 logits, hs = self.step(x, hs, m_t, a_t)
                 if record_logits is not None and i in record_logits:
                     logits_rec[i] = logits.clone().numpy()
-                if self.mode == 'MOL':
+                if self.beta:
+                    # vocoder/distribution.py:7-20 with Beta(alpha, beta).sample() on the
+                    # Philox BETA contract: alpha, beta = exp(logits) in fp32
+                    loc = logits.exp()
+                    sample = torch.from_numpy(philox.beta_sample(
+                        seed, stream, i, rows, loc[:, 0].numpy(), loc[:, 1].numpy()))
+                    samples.append(sample)
+                    x = sample.unsqueeze(-1)
+                elif self.mode == 'MOL':
                     u1, u2 = philox.mol_uniforms(seed, stream, [i], rows)
                     sample, _ = self.sample_mol(logits.unsqueeze(0).transpose(1, 2),
                                                 torch.from_numpy(u1), torch.from_numpy(u2))
@@ -315,7 +324,7 @@ class OracleWaveRNN:
                     progress_callback(i, seq_len, b_size, gen_rate)
             out['t_loop'] = time.time() - t0
         out['B'], out['S'], out['steps'] = b_size, seq_len, n_steps
-        out['labels'] = labels if self.mode != 'MOL' else None
+        out['labels'] = labels if self.mode != 'MOL' and not self.beta else None
         output = torch.stack(samples).transpose(0, 1)
         out['samples'] = output.numpy().copy()
         out['logits'] = logits_rec

@@ -21,6 +21,7 @@
 // then, redundantly in every workgroup, the sample and GRU1 of the next step (rank-1 x term).
 #include "wrnn_kernels.h"
 #include "persist_common.h"
+#include "philox.h"
 
 namespace wrnn {
 
@@ -78,7 +79,7 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
 
 }  // namespace
 
-template <int NR>
+template <int NR, bool BETA>
 __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -334,6 +335,20 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                     }
                 }
             }
+        } else if (BETA) {
+            // BETA (geneing 'RAW'): vocoder/distribution.py:7-20, Beta(exp l0, exp l1) on [-1, 1]
+            // with the Philox gamma draws (philox.h beta_sample), one lane per row
+            if (tid < NR) {
+                const int r = tid, row = g0 + kPG * r;
+                const unsigned lo = (unsigned)(r * 32) * 4u;
+                const unsigned so = (QX_D + QX_D_LOG) * 4;
+                const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[r];
+                const float al = expf(bld_nt(xr, lo, so)), be = expf(bld_nt(xr, lo + 4u, so));
+                const float xv = beta_sample(al, be, (uint32_t)t, (uint32_t)lri.fold, lri.stream,
+                                             a.k0, a.k1);
+                lds[L_SX + r] = xv;
+                if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+            }
         } else if (tid < NR) {
             // MOL: vocoder/distribution.py:104-140 with the precomputed draws of k_mol_noise
             const int r = tid, row = g0 + kPG * r;
@@ -424,51 +439,63 @@ size_t persist_gen_lds_bytes() {
 }
 size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
 
-template <int NR>
+// BETA (geneing 'RAW') is its own instantiation: its float64 gamma sampler would otherwise
+// raise the register allocation of the RAW / MOL variants
+template <int NR, bool BETA>
 hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
     static bool attr = false;
     const size_t lds = persist_gen_lds_bytes();
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR, BETA>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_persist_gen<NR>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    hipLaunchKernelGGL((k_persist_gen<NR, BETA>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int NR>
+template <int NR, bool BETA>
 int persist_gen_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, BETA>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
-int persist_gen_variant_ok(int nr, int cpw) {
-    if (cpw < 1 || cpw > 32) return 0;
-    int sp = -1;
+template <bool BETA>
+int persist_gen_spill_nr(int nr) {
     switch (nr) {
-        case 1: sp = persist_gen_spill_t<1>(); break;
-        case 2: sp = persist_gen_spill_t<2>(); break;
-        case 3: sp = persist_gen_spill_t<3>(); break;
-        case 4: sp = persist_gen_spill_t<4>(); break;
-        default: break;
+        case 1: return persist_gen_spill_t<1, BETA>();
+        case 2: return persist_gen_spill_t<2, BETA>();
+        case 3: return persist_gen_spill_t<3, BETA>();
+        case 4: return persist_gen_spill_t<4, BETA>();
+        default: return -1;
     }
-    return sp == 0 ? 1 : 0;
+}
+
+int persist_gen_variant_ok(int nr, int cpw, int mode) {
+    if (cpw < 1 || cpw > 32) return 0;
+    // (the BETA variants keep a small stack frame for the float64 trig range reduction)
+    const int sp = mode == 2 ? persist_gen_spill_nr<true>(nr) : persist_gen_spill_nr<false>(nr);
+    return sp >= 0 && sp <= (mode == 2 ? 16 : 0) ? 1 : 0;
+}
+
+template <bool BETA>
+hipError_t launch_persist_gen_m(const PersistGenArgs& a, hipStream_t s) {
+    switch (a.nr) {
+        case 1: return launch_persist_gen_t<1, BETA>(a, s);
+        case 2: return launch_persist_gen_t<2, BETA>(a, s);
+        case 3: return launch_persist_gen_t<3, BETA>(a, s);
+        case 4: return launch_persist_gen_t<4, BETA>(a, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > 32 ||
         a.cpw * kPM < a.n_classes || (a.mode != 0 && a.n_classes > 32))
         return hipErrorInvalidValue;
-    switch (a.nr) {
-        case 1: return launch_persist_gen_t<1>(a, s);
-        case 2: return launch_persist_gen_t<2>(a, s);
-        case 3: return launch_persist_gen_t<3>(a, s);
-        case 4: return launch_persist_gen_t<4>(a, s);
-        default: return hipErrorInvalidValue;
-    }
+    return a.mode == 2 ? launch_persist_gen_m<true>(a, s) : launch_persist_gen_m<false>(a, s);
 }
 
 }  // namespace wrnn

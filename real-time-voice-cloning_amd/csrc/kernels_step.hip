@@ -506,6 +506,17 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
                 a.labels[(size_t)r * a.S + a.t] = (int16_t)bk;
                 a.samples[(size_t)r * a.S + a.t] = x;
             }
+        } else if (a.mode == 2) {
+            // BETA (geneing 'RAW'): vocoder/distribution.py:7-20, Beta(exp l0, exp l1) on [-1, 1]
+            if (tid == 0) {
+                const float* lg = a.logits + (size_t)r * n;
+                const float xv = beta_sample(expf(lg[0]), expf(lg[1]), (uint32_t)a.t,
+                                             (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+                a.samples[(size_t)r * a.S + a.t] = xv;
+                xsh = xv;
+            }
+            __syncthreads();
+            x = xsh;
         } else {
             // MOL: vocoder/distribution.py:104-140 with the Philox draws
             const float* lg = a.logits + (size_t)r * n;

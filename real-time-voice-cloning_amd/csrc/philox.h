@@ -45,4 +45,53 @@ __host__ __device__ inline float mol_uniform_from_u32(uint32_t x) {
 
 constexpr uint32_t kMolDomain = 0x80000000u;
 
+// BETA: geneing 'RAW' mode (vocoder/distribution.py:7-20, Beta(exp(l0), exp(l1)).sample()) on
+// the stream: X / (X + Y) with X ~ Gamma(alpha), Y ~ Gamma(beta) by Marsaglia-Tsang in float64
+// (oracle/philox.py gamma_mt / beta_sample, same operation order, contraction off).
+constexpr uint32_t kBetaDomain = 0x40000000u;
+constexpr int kBetaTries = 16;
+
+__host__ __device__ inline double u_open_from_u32(uint32_t x) {
+    return (2.0 * (double)(x >> 9) + 1.0) * (1.0 / 16777216.0);
+}
+
+__host__ __device__ inline double gamma_mt(double a, uint32_t g, uint32_t step, uint32_t row,
+                                           uint32_t stream, uint32_t k0, uint32_t k1) {
+#pragma clang fp contract(off)
+    const bool boost = a < 1.0;
+    const double ap = boost ? a + 1.0 : a;
+    const double d = ap - 1.0 / 3.0;
+    const double c = 1.0 / sqrt(9.0 * d);
+    double out = d, ub = 1.0;
+    for (int k = 0; k < kBetaTries; ++k) {
+        const U4 w = philox4x32_10(kBetaDomain | (g << 8) | (uint32_t)k, step, row, stream, k0, k1);
+        const double u0 = u_open_from_u32(w.x), u1 = u_open_from_u32(w.y);
+        const double u2 = u_open_from_u32(w.z), u3 = u_open_from_u32(w.w);
+        const double z = sqrt(-2.0 * log(u0)) * cos((2.0 * 3.141592653589793) * u1);
+        const double t = 1.0 + c * z;
+        const double v = (t * t) * t;
+        if (v > 0.0) {
+            const double rhs = ((0.5 * z) * z + d - d * v) + d * log(v);
+            if (log(u2) < rhs) {
+                out = d * v;
+                ub = u3;
+                break;
+            }
+        }
+    }
+    if (boost) out = out * pow(ub, 1.0 / a);
+    const double tiny = 2.2250738585072014e-308;  // DBL_MIN
+    return out > tiny ? out : tiny;
+}
+
+// Beta(alpha, beta) rescaled to [-1, 1] in float32 (the reference's 2.0 * sample - 1.0)
+__host__ __device__ inline float beta_sample(float alpha, float beta, uint32_t step, uint32_t row,
+                                             uint32_t stream, uint32_t k0, uint32_t k1) {
+#pragma clang fp contract(off)
+    const double x = gamma_mt((double)alpha, 0u, step, row, stream, k0, k1);
+    const double y = gamma_mt((double)beta, 1u, step, row, stream, k0, k1);
+    const float s = (float)(x / (x + y));
+    return 2.0f * s - 1.0f;
+}
+
 }  // namespace wrnn

@@ -1308,13 +1308,13 @@ void phase_report(wrnn_handle* h) {
 }
 
 // A noise-seed-dependent kernel argument (MOL Philox key) is baked into captured graphs, so the
-// cache key includes it through `timing` only when RAW; MOL graphs are keyed by seed below.
+// cache key includes it through `timing` only when RAW; MOL / BETA graphs are keyed by seed below.
 int run_chunk(wrnn_handle* h, int t0, int len, int S) {
     const bool last = t0 + len >= S;
     const int key_S = last ? S : -1;
     auto key = std::make_tuple(t0, len, key_S, h->last_B,
                                (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1),
-                               h->cfg.mode == WRNN_MODE_MOL ? h->seed : (uint64_t)0);
+                               h->cfg.mode != WRNN_MODE_RAW ? h->seed : (uint64_t)0);
     auto it = h->graphs.find(key);
     if (it == h->graphs.end()) {
         hipGraph_t g;
@@ -1545,6 +1545,10 @@ int persist_noise(wrnn_handle* h, int S, hipStream_t st) {
     auto& P = h->pws;
     const int Bp = h->last_Bp, n = h->n_classes;
     const bool raw = h->cfg.mode == WRNN_MODE_RAW;
+    if (h->cfg.mode == WRNN_MODE_BETA) {  // gamma draws are made in-kernel
+        CHECK(P.gumbel.alloc(sizeof(float)));
+        return WRNN_OK;
+    }
     CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
     const RowInfo* rows = (const RowInfo*)h->ws.rows.p;
@@ -1649,6 +1653,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         ag.samples = a.samples;
         ag.ld = a.ld;
         ag.st = P.st.f();
+        ag.k0 = (uint32_t)(h->seed & 0xffffffffu);
+        ag.k1 = (uint32_t)(h->seed >> 32);
         HIPC(launch_persist_gen_init(ag, st));
     } else if (rr) {
         ar.ctl = a.ctl;
@@ -1909,7 +1915,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             }
         } else {
             for (int r = kPNR; r >= 1; --r)
-                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw) : persist_rr_variant_ok(r, h->pw.cpw)) {
+                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw)) {
                     opts.push_back({r, false, 1.0});  // one launch per batch of the largest variant
                     break;
                 }
@@ -2146,8 +2152,10 @@ int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
     if (cfg->model_type != WRNN_MODEL_FATCHORD && cfg->model_type != WRNN_MODEL_RUNTIMERACER &&
         cfg->model_type != WRNN_MODEL_GENEING)
         return fail(WRNN_ERR_INVALID, "Invalid model type " + std::to_string(cfg->model_type));
-    if (cfg->mode != WRNN_MODE_RAW && cfg->mode != WRNN_MODE_MOL)
+    if (cfg->mode != WRNN_MODE_RAW && cfg->mode != WRNN_MODE_MOL && cfg->mode != WRNN_MODE_BETA)
         return fail(WRNN_ERR_INVALID, "Unknown model mode value - " + std::to_string(cfg->mode));
+    if (cfg->mode == WRNN_MODE_BETA && cfg->model_type != WRNN_MODEL_GENEING)
+        return fail(WRNN_ERR_INVALID, "BETA mode is the geneing 'RAW' head only");
     if (cfg->mode == WRNN_MODE_RAW && (cfg->bits < 2 || cfg->bits > 12))
         return fail(WRNN_ERR_INVALID, "bits must be in [2, 12]");
     if (cfg->n_upsample < 1 || cfg->n_upsample > 4)
@@ -2170,7 +2178,7 @@ int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
     h->R = cfg->res_out_dims;
     h->feat = cfg->feat_dims;
     h->hop = cfg->hop_length;
-    h->n_classes = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : 30;
+    h->n_classes = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : cfg->mode == WRNN_MODE_BETA ? 2 : 30;
     h->n_gru = cfg->model_type == WRNN_MODEL_FATCHORD ? 2 : cfg->model_type == WRNN_MODEL_GENEING ? 1 : 4;
     h->indent = cfg->pad * prod;
     build_expected(h.get());
@@ -2389,6 +2397,15 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
     }
     if (bytes) *bytes = by;
     if (flops) *flops = fl;
+    return WRNN_OK;
+}
+
+int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,
+                    float beta, float* out) {
+    if (!out) return fail(WRNN_ERR_INVALID, "null argument");
+    if (!(alpha > 0.f) || !(beta > 0.f)) return fail(WRNN_ERR_INVALID, "alpha, beta must be > 0");
+    *out = beta_sample(alpha, beta, step, row, stream, (uint32_t)(seed & 0xffffffffu),
+                       (uint32_t)(seed >> 32));
     return WRNN_OK;
 }
 

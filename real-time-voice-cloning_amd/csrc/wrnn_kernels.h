@@ -298,12 +298,13 @@ struct PersistGenArgs {
     float* st;              // chunk state [B][2 H]: x1, h1
     uint32_t* stamps;
     unsigned* progress;     // as PersistArgs
+    uint32_t k0, k1;        // Philox key (BETA draws in-kernel)
     int prog_base;
 };
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s);
 hipError_t launch_persist_gen_init(const PersistGenArgs& a, hipStream_t s);
-int persist_gen_variant_ok(int nr, int cpw);
+int persist_gen_variant_ok(int nr, int cpw, int mode);
 size_t persist_gen_lds_bytes();
 size_t persist_gen_xbuf_floats();
 hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s);

@@ -67,18 +67,19 @@ class WaveRNN:
             raise NotImplementedError("Invalid model of type '%s' provided. Aborting..." % model_type)
         geneing = model_type == MODEL_TYPE_GENEING
         if geneing and mode == 'RAW':
-            # geneing_version.py:95-96,207-210: RAW = 2 Beta parameters; torch's Beta sampler
-            # (rejection-sampled gammas) has no noise contract here
-            raise NotImplementedError("geneing-wavernn mode 'RAW' (Beta sampling) is not supported; "
-                                      "use 'BITS' or 'MOL'")
-        if mode == 'RAW' or (geneing and mode == 'BITS'):
+            # geneing_version.py:95-96,207-210: 2 outputs, Beta(exp l0, exp l1) on [-1, 1]
+            self.n_classes = 2
+        elif mode == 'RAW' or (geneing and mode == 'BITS'):
             self.n_classes = 2 ** bits
         elif mode == 'MOL':
             self.n_classes = 30
         else:
             raise RuntimeError("Unknown model mode value - ", mode)
-        # categorical sampling over n_classes: RAW (fatchord / runtimeracer) and geneing BITS
-        self.categorical = mode != 'MOL'
+        # categorical sampling over n_classes: RAW (fatchord / runtimeracer) and geneing BITS;
+        # continuous samples: MOL and geneing RAW (Beta)
+        self.categorical = mode != 'MOL' and not (geneing and mode == 'RAW')
+        self._dev_mode = (_abi.WRNN_MODE_RAW if self.categorical else
+                          _abi.WRNN_MODE_BETA if mode == 'RAW' else _abi.WRNN_MODE_MOL)
         self.mode = mode
         self.bits = bits
         self.pad = pad
@@ -94,7 +95,7 @@ class WaveRNN:
         self._lib = _abi.load_library()
         cfg = _abi.WrnnConfig()
         cfg.model_type = _MODEL_IDS[model_type]
-        cfg.mode = _abi.WRNN_MODE_RAW if self.categorical else _abi.WRNN_MODE_MOL
+        cfg.mode = self._dev_mode
         cfg.bits = bits
         cfg.rnn_dims, cfg.fc_dims = rnn_dims, fc_dims
         cfg.compute_dims, cfg.res_out_dims = compute_dims, res_out_dims
@@ -337,7 +338,7 @@ class WaveRNN:
     def postprocess_rows(self, rows, n_frames, batched, target, overlap, mu_law,
                          apply_preemphasis):
         """Host f64 post-processing of one utterance's fold rows (fatchord_version.py:238-255):
-        ``rows`` (num_folds, S) int16 labels (categorical) or float32 samples (MOL)."""
+        ``rows`` (num_folds, S) int16 labels (categorical) or float32 samples (MOL, Beta)."""
         mu_law = mu_law if self.mode == 'RAW' else False
         wave_len = (int(n_frames) - 1) * self.hop_length
         if self.categorical and batched:

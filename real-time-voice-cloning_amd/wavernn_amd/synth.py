@@ -19,7 +19,11 @@ MODEL_TYPE_RUNTIMERACER = 'runtimeracer-wavernn'
 MODEL_TYPE_GENEING = 'geneing-wavernn'
 
 
-def n_classes_of(hp):
+def n_classes_of(hp, model_type=None):
+    """fc3 outputs: geneing 'RAW' = 2 Beta parameters (geneing_version.py:95-96), RAW / BITS
+    = 2**bits classes, MOL = 30."""
+    if model_type == MODEL_TYPE_GENEING and hp.mode == 'RAW':
+        return 2
     return 2 ** hp.bits if hp.mode in ('RAW', 'BITS') else 30
 
 
@@ -50,7 +54,7 @@ def state_dict_spec(hp, model_type, feat_dims=80):
         spec[f'upsample.up_layers.{2 * j + 1}.weight'] = (1, 1, 1, 2 * s + 1)
     H, F = hp.rnn_dims, hp.fc_dims
     A = aux_dims_of(hp, model_type)
-    n = n_classes_of(hp)
+    n = n_classes_of(hp, model_type)
     spec['I.weight'] = (H, feat_dims + A)
     spec['I.bias'] = (H,)
 

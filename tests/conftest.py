@@ -27,6 +27,11 @@ def golden_case(name):
     return golden_meta()[name], dict(np.load(os.path.join(GOLDEN, name + '.npz')))
 
 
+def is_continuous(meta):
+    """Float samples (MOL, geneing 'RAW' Beta) rather than categorical labels."""
+    return meta['mode'] == 'MOL' or (meta['model_type'] == 'geneing-wavernn' and meta['mode'] == 'RAW')
+
+
 def hparams_of(meta):
     from wavernn_amd.hparams import wavernn_fatchord, wavernn_geneing, wavernn_runtimeracer
     base = {'fatchord-wavernn': wavernn_fatchord, 'geneing-wavernn': wavernn_geneing,

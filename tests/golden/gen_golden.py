@@ -59,6 +59,9 @@ CASES = {
                          [0, 2]),
     'geneing_bits9_defaults': ('geneing-wavernn', 'BITS', 9, 53, True, None, None, 11, 21, 1.0,
                                111, [0]),
+    # geneing 'RAW' = Beta sampling (geneing_version.py:207-210, distribution.py:7-20)
+    'geneing_raw_beta_tiny': ('geneing-wavernn', 'RAW', 10, 24, True, 1000, 100, 12, 22, 1.0, 112,
+                              [0, 1, 700]),
     # BASELINE.json configs[0]: 200-frame random mel, mu-law 9-bit, target=11000 overlap=550
     'fatchord_raw9_config1': ('fatchord-wavernn', 'RAW', 9, 200, True, 11000, 550, 0, 0, 1.0, 0,
                               [0, 1, 6000, 12099]),
@@ -146,6 +149,25 @@ def make_mol_patch(orig):
     return patched
 
 
+def make_beta_patch():
+    """vocoder/distribution.py:7-20 with the Beta draw on the Philox BETA contract: the
+    reference's own fp32 exp() of the two parameters, the sample rescaled by the reference's
+    own fp32 2.0 * sample - 1.0."""
+    def patched(y_hat):
+        loc_y = y_hat.exp()
+        B = y_hat.size(1)
+        alpha = loc_y[:, :, 0].unsqueeze(-1)
+        beta = loc_y[:, :, 1].unsqueeze(-1)
+        x = philox.gamma_mt(NoiseState.seed, NoiseState.stream, NoiseState.step, np.arange(B),
+                            alpha.reshape(-1).numpy().astype(np.float64), 0)
+        y = philox.gamma_mt(NoiseState.seed, NoiseState.stream, NoiseState.step, np.arange(B),
+                            beta.reshape(-1).numpy().astype(np.float64), 1)
+        sample = torch.from_numpy((x / (x + y)).astype(np.float32)).view(1, B, 1)
+        NoiseState.step += 1
+        return 2.0 * sample - 1.0
+    return patched
+
+
 def ref_hparams(model_type, mode, bits):
     from config import hparams as H
     import copy
@@ -210,6 +232,8 @@ def run_reference(name, case):
     torch.distributions.Categorical = PatchedCategorical
     fv_orig, rv_orig = fv.sample_from_discretized_mix_logistic, rv.sample_from_discretized_mix_logistic
     gv_orig = gv.sample_from_discretized_mix_logistic
+    gv_beta = gv.sample_from_beta_dist
+    gv.sample_from_beta_dist = make_beta_patch()
     fv.sample_from_discretized_mix_logistic = make_mol_patch(fv_orig)
     rv.sample_from_discretized_mix_logistic = make_mol_patch(rv_orig)
     gv.sample_from_discretized_mix_logistic = make_mol_patch(gv_orig)
@@ -232,13 +256,14 @@ def run_reference(name, case):
         fv.sample_from_discretized_mix_logistic = fv_orig
         rv.sample_from_discretized_mix_logistic = rv_orig
         gv.sample_from_discretized_mix_logistic = gv_orig
+        gv.sample_from_beta_dist = gv_beta
         hnd.remove()
     dt = time.time() - t0
     model.eval()
     samples = captured['samples']
     res = dict(wav=np.asarray(wav, dtype=np.float64), samples=samples.astype(np.float32),
                steps=NoiseState.step, t=dt)
-    if mode != 'MOL':
+    if mode != 'MOL' and not (model_type == 'geneing-wavernn' and mode == 'RAW'):
         n = 2 ** bits
         # labels recovered exactly from the fp32 samples: sample = 2k/(n-1) - 1 (fp32)
         ks = np.arange(n, dtype=np.float32)
@@ -278,7 +303,8 @@ def main():
         t_or = time.time() - t0
         same_wav = np.array_equal(o['wav'], res['wav'])
         same_samples = np.array_equal(o['samples'], res['samples'])
-        same_labels = (mode == 'MOL') or np.array_equal(o['labels'], res['labels'])
+        continuous = mode == 'MOL' or (model_type == 'geneing-wavernn' and mode == 'RAW')
+        same_labels = continuous or np.array_equal(o['labels'], res['labels'])
         same_logits = all(np.array_equal(o['logits'][s], res['logits'][s]) for s in rec_steps)
         print(f"{name}: B={o['B']} S={o['S']} ref {res['t']:.1f}s oracle {t_or:.1f}s "
               f"wav_eq={same_wav} samples_eq={same_samples} labels_eq={same_labels} "
@@ -286,7 +312,7 @@ def main():
         assert same_wav and same_samples and same_labels and same_logits, name
         out = dict(wav=res['wav'], logits_steps=np.array(rec_steps, dtype=np.int64),
                    logits=np.stack([res['logits'][s] for s in rec_steps]).astype(np.float32))
-        if mode != 'MOL':
+        if not continuous:
             out['labels'] = res['labels']
         else:
             out['samples'] = res['samples']

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -67,3 +68,31 @@ def test_product_fails_loudly_without_library(tmp_path):
     from wavernn_amd import _abi
     with pytest.raises(_abi.NativeLibraryMissing):
         _abi.load_library(str(tmp_path / 'missing.so'))
+
+
+def test_beta_contract_host_restatement_matches_oracle():
+    """wrnn_debug_beta evaluates csrc/philox.h beta_sample (the code the kernels run) on the
+    host; it must agree with oracle/philox.py beta_sample for shapes below and above 1."""
+    from oracle import philox
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    rng = np.random.default_rng(3)
+    out = ctypes.c_float()
+    for i in range(300):
+        a, b = np.exp(rng.uniform(-3, 4, 2)).astype(np.float32)
+        seed, stream, step, row = int(rng.integers(0, 2 ** 63)), i % 5, 17 * i, i % 7
+        assert lib.wrnn_debug_beta(seed, stream, step, row, float(a), float(b),
+                                   ctypes.byref(out)) == 0
+        ref = philox.beta_sample(seed, stream, step, [row], np.float32([a]), np.float32([b]))[0]
+        assert abs(out.value - float(ref)) <= 2e-6, (a, b, out.value, ref)
+    assert lib.wrnn_debug_beta(0, 0, 0, 0, 0.0, 1.0, ctypes.byref(out)) == _abi.WRNN_ERR_INVALID
+
+
+def test_beta_mode_is_geneing_only():
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    cfg = _abi.WrnnConfig()
+    cfg.model_type, cfg.mode = _abi.WRNN_MODEL_FATCHORD, _abi.WRNN_MODE_BETA
+    h = ctypes.c_void_p()
+    assert lib.wrnn_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == _abi.WRNN_ERR_INVALID
+    assert b'geneing' in lib.wrnn_last_error()

@@ -1,12 +1,12 @@
 """GPU parity: the HIP path (through the C-ABI) against the reference's golden outputs and the
 oracle restatement. Bar (BASELINE.json north_star): RAW 9/10-bit labels bit-exact, waveform
-bit-exact (f64 post-processing is the reference's own numpy/scipy code); MOL float path within
-1e-4 RMS.
+bit-exact (f64 post-processing is the reference's own numpy/scipy code); MOL and geneing 'RAW'
+(Beta) float paths within 1e-4 RMS.
 """
 import numpy as np
 import pytest
 
-from conftest import golden_case, golden_meta, hparams_of
+from conftest import golden_case, golden_meta, hparams_of, is_continuous
 
 pytestmark = pytest.mark.gpu
 
@@ -47,20 +47,20 @@ def first_divergence(a, b):
     return None if len(d) == 0 else tuple(d[np.argmin(d[:, 1])])
 
 
-def engine_cases(*modes):
+def engine_cases(continuous):
     # both engines run every topology (PERSIST: kernels_persist.hip fatchord,
     # kernels_persist_rr.hip runtimeracer, kernels_persist_gen.hip geneing)
     out = []
     for k, v in golden_meta().items():
-        if v['mode'] not in modes:
+        if is_continuous(v) != continuous:
             continue
         out.append((k, 'chain'))
         out.append((k, 'persist'))
     return out
 
 
-RAW_CASES = engine_cases('RAW', 'BITS')  # geneing 'BITS' = categorical over 2**bits classes
-MOL_CASES = engine_cases('MOL')
+RAW_CASES = engine_cases(False)  # RAW and geneing 'BITS': categorical over 2**bits classes
+MOL_CASES = engine_cases(True)   # MOL and geneing 'RAW' (Beta): float samples
 
 
 @pytest.mark.parametrize('name,engine', RAW_CASES)
@@ -150,9 +150,10 @@ def test_persist_multi_row_groups_match_oracle(n_utts, case):
             f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'
 
 
-@pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny', 'geneing_mol_tiny'])
+@pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny', 'geneing_mol_tiny',
+                                  'geneing_raw_beta_tiny'])
 def test_persist_row_batches_mol_within_tolerance(case):
-    """MOL float path over row batches (6 utterances x the case's fold rows)."""
+    """MOL / Beta float path over row batches (6 utterances x the case's fold rows)."""
     import torch
     from oracle.wavernn_oracle import oracle_infer_waveform
     from wavernn_amd.hparams import sp

@@ -4,7 +4,7 @@ survey container with the reference imported from /root/reference). CPU only."""
 import numpy as np
 import pytest
 
-from conftest import golden_case, golden_meta, hparams_of
+from conftest import golden_case, golden_meta, hparams_of, is_continuous
 
 FAST = [k for k, v in golden_meta().items() if v['seq_len'] * v['num_folds'] <= 25000]
 SLOW = [k for k in golden_meta() if k not in FAST]
@@ -28,7 +28,7 @@ def run_oracle(name):
 def check(name):
     meta, gold, o = run_oracle(name)
     assert (o['B'], o['S']) == (meta['num_folds'], meta['seq_len'])
-    if meta['mode'] != 'MOL':  # RAW / geneing BITS: categorical labels
+    if not is_continuous(meta):  # RAW / geneing BITS: categorical labels
         assert np.array_equal(o['labels'], gold['labels'])
     else:
         assert np.array_equal(o['samples'], gold['samples'])

@@ -39,3 +39,26 @@ def test_mol_uniforms_range():
     assert u1.shape == (100, 3, 10) and u2.shape == (100, 3)
     for u in (u1, u2):
         assert (u >= np.float32(1e-5)).all() and (u <= np.float32(1 - 1e-5)).all()
+
+
+def test_beta_samples_follow_beta_distribution():
+    """BETA contract (geneing 'RAW', vocoder/distribution.py:7-20): 2 Beta(a, b) - 1 with the
+    right first two moments, for shapes above and below 1 (the a < 1 boost path)."""
+    rows = np.arange(20000)
+    for a, b in ((2.0, 5.0), (0.5, 0.7), (30.0, 3.0), (1.0, 1.0)):
+        x = philox.beta_sample(11, 2, 7, rows, np.full(rows.shape, a, np.float32),
+                               np.full(rows.shape, b, np.float32)).astype(np.float64)
+        assert ((x >= -1) & (x <= 1)).all()
+        s = (x + 1) / 2
+        mean, var = a / (a + b), a * b / ((a + b) ** 2 * (a + b + 1))
+        assert abs(s.mean() - mean) < 5 * np.sqrt(var / len(rows)) + 1e-4, (a, b)
+        assert abs(s.var() - var) < 0.05 * var, (a, b)
+
+
+def test_beta_streams_are_distinct_and_reproducible():
+    al = np.full(4, 2.0, np.float32)
+    x = philox.beta_sample(1, 0, 5, np.arange(4), al, al)
+    assert np.array_equal(x, philox.beta_sample(1, 0, 5, np.arange(4), al, al))
+    assert len(set(x.tolist())) == 4
+    assert not np.array_equal(x, philox.beta_sample(1, 1, 5, np.arange(4), al, al))
+    assert not np.array_equal(x, philox.beta_sample(1, 0, 6, np.arange(4), al, al))

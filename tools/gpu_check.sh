@@ -16,7 +16,7 @@ run() {  # run <name> <timeout> cmd...
 }
 STEPS=${STEPS:-parity,smoke,bench}
 [[ ,$STEPS, == *,parity,* ]] && run parity 600 python -m pytest tests/test_gpu_parity.py -q -x -rA ${PARITY_ARGS:-}
-[[ ,$STEPS, == *,gputests,* ]] && run gputests 1000 python -u -m pytest tests -m gpu -v -rA --timeout 240 --timeout-method thread ${GPUTEST_ARGS:-}
+[[ ,$STEPS, == *,gputests,* ]] && run gputests 1000 python -u -m pytest tests -m gpu -v -rA --timeout 240 --timeout-method thread -k "${GPUTEST_K:-}" ${GPUTEST_ARGS:-}
 [[ ,$STEPS, == *,phase,* ]] && run phase 300 env WRNN_PHASE_STEP=${PHASE_STEP:-600} python bench.py --steps 1 --warmup 0 --cpu-seconds 0
 [[ ,$STEPS, == *,smoke,* ]] && run smoke 300 python __graft_entry__.py smoke
 [[ ,$STEPS, == *,bench,* ]] && run bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds ${CPU_SECONDS:-10}
