@@ -2,8 +2,13 @@
 //
 // Format written by the reference's vocoder/libwavernn/convert.py:38-58 (file header),
 // :60-81 (1x4 block-compressed matrices), :83-156 (per-layer records), :303-351 (layer order);
-// read by libwavernn/<variant>/src/wavernn.cpp:37-184. All integers are native int32, floats
-// are fp32 ("elSize" 4), structs packed with Python's '@' (native) layout:
+// read by libwavernn/<variant>/src/wavernn.cpp:37-184. All integers are native int32; the
+// arrays of a layer are fp32 ("elSize" 4) or IEEE binary16 ("elSize" 2, convert.py:12 "change
+// to 2 for fp16"; widened to fp32 on load), the BatchNorm eps is always fp32; structs packed
+// with Python's '@' (native) layout. (The reference's C++ reader accepts elSize 2 but freads
+// the 2-byte elements straight into fp32 storage, wavernn.h:83 / wavernn.cpp:103, and its
+// convert.py writes fp32 payloads whatever the header says, so no reference output exists for
+// an fp16 file: here elSize 2 means what the header comment declares.)
 //   header   int32 res_blocks, n_upsample, total_scale, pad
 //   layer    int32 type (1 Conv1d, 2 Conv2d, 3 BatchNorm1d, 4 Linear, 5 GRU, 6 Stretch2d),
 //            char name[64] (the module's repr), then the type's record:
@@ -35,9 +40,33 @@ int bfail(int code, const std::string& msg) { return wrnn_internal_fail(code, ms
 
 constexpr int kGroup = 4;  // hparams sparse_group (config/hparams.py) used by convert.py
 
+// IEEE binary16 -> binary32 (exact: every half is a float)
+float half_to_float(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu, bits;
+    if (e == 0x1f) {
+        bits = sign | 0x7f800000u | (m << 13);  // inf / nan
+    } else if (e != 0) {
+        bits = sign | ((e + 112u) << 23) | (m << 13);
+    } else if (m == 0) {
+        bits = sign;
+    } else {  // subnormal: normalise
+        int sh = 0;
+        while (!(m & 0x400u)) {
+            m <<= 1;
+            ++sh;
+        }
+        bits = sign | ((uint32_t)(113 - sh) << 23) | ((m & 0x3ffu) << 13);
+    }
+    float f;
+    std::memcpy(&f, &bits, 4);
+    return f;
+}
+
 struct Reader {
     const uint8_t* p;
     size_t n, off = 0;
+    int es = 4;  // element size of the current layer's arrays
     std::string err;
     bool take(void* dst, size_t k) {
         if (!err.empty()) return false;
@@ -61,12 +90,22 @@ struct Reader {
     }
     std::vector<float> floats(int64_t k) {
         std::vector<float> v;
-        if (k < 0 || (uint64_t)k * 4 > n - off) {
-            if (err.empty()) err = "bad array length " + std::to_string(k) + " at byte " + std::to_string(off);
+        if (!err.empty()) return v;
+        if (k < 0 || (uint64_t)k * es > n - off) {
+            err = "bad array length " + std::to_string(k) + " at byte " + std::to_string(off);
             return v;
         }
         v.resize((size_t)k);
-        take(v.data(), (size_t)k * 4);
+        if (es == 4) {
+            take(v.data(), (size_t)k * 4);
+        } else {
+            for (int64_t i = 0; i < k; ++i) {
+                uint16_t h;
+                std::memcpy(&h, p + off + 2 * (size_t)i, 2);
+                v[(size_t)i] = half_to_float(h);
+            }
+            off += (size_t)k * 2;
+        }
         return v;
     }
 };
@@ -99,9 +138,11 @@ bool layer_header(Reader& r, int want) {
     return true;
 }
 
-bool el_size(Reader& r) {
+bool el_size(Reader& r) {  // wavernn.cpp:98 `assert(header.elSize==4 or header.elSize==2)`
     const int e = r.i32();
-    if (r.err.empty() && e != 4) r.err = "elSize " + std::to_string(e) + " (only fp32 files are supported)";
+    if (r.err.empty() && e != 4 && e != 2)
+        r.err = "elSize " + std::to_string(e) + " at byte " + std::to_string(r.off - 4) + " (4 = fp32, 2 = fp16)";
+    r.es = e == 2 ? 2 : 4;
     return r.err.empty();
 }
 
@@ -242,7 +283,7 @@ extern "C" int wrnn_bin_read(const void* data, size_t bytes, const wrnn_config* 
                                   std::to_string(pad) + ") does not match the model configuration");
     const int C = cfg->compute_dims, R = cfg->res_out_dims, F0 = cfg->feat_dims, H = cfg->rnn_dims,
               Fc = cfg->fc_dims, k_in = 2 * cfg->pad + 1;
-    const int n = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : 30;
+    const int n = cfg->mode == WRNN_MODE_RAW ? (1 << cfg->bits) : cfg->mode == WRNN_MODE_BETA ? 2 : 30;
     // MelResNet (convert.py:310-320)
     conv1d(r, E, "upsample.resnet.conv_in", F0, C, k_in, false);
     batchnorm(r, E, "upsample.resnet.batch_norm", C);

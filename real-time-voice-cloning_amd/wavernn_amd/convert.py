@@ -9,6 +9,10 @@ loaded back into this build (``wrnn_bin_read`` / ``wrnn_load_bin`` in the C-ABI 
 The writer works from a state dict (numpy or torch tensors), not from ``nn.Module`` objects;
 the module repr that the reference stores in each 64-byte layer name field is informational
 (the C++ reader skips it) and is written as the module's class name here.
+
+``el_size`` 2 writes every layer's arrays as IEEE binary16 (the reference's ``elSize = 4
+#change to 2 for fp16``, convert.py:12); the reader widens them to fp32 on load. The
+BatchNorm eps stays fp32 as in the reference's ``'@iif'`` record.
 """
 import ctypes
 import struct
@@ -45,14 +49,20 @@ def compress(W, group=SPARSE_GROUP):
 
 
 class _Writer:
-    def __init__(self, f):
+    def __init__(self, f, el_size=EL_SIZE):
+        if el_size not in (4, 2):
+            raise ValueError('el_size must be 4 (fp32) or 2 (fp16)')
         self.f = f
+        self.el = el_size
 
     def raw(self, fmt, *v):
         self.f.write(struct.pack(fmt, *v))
 
     def arr(self, a):
-        self.f.write(_np(a).tobytes(order='C'))
+        a = _np(a)
+        if self.el == 2:
+            a = a.astype(np.float16)
+        self.f.write(a.tobytes(order='C'))
 
     def layer(self, kind, name):
         self.raw('@i64s', LAYER_IDS[kind], name.encode()[:64])
@@ -68,7 +78,7 @@ class _Writer:
         W = _np(sd[p + '.weight'])
         out_ch, in_ch, k = W.shape
         self.layer('Conv1d', 'Conv1d')
-        self.raw('@iiiii', EL_SIZE, int(bias), in_ch, out_ch, k)
+        self.raw('@iiiii', self.el, int(bias), in_ch, out_ch, k)
         self.arr(W)
         if bias:
             self.arr(sd[p + '.bias'])
@@ -76,14 +86,14 @@ class _Writer:
     def batchnorm(self, sd, p, eps=1e-5):
         w = _np(sd[p + '.weight'])
         self.layer('BatchNorm1d', 'BatchNorm1d')
-        self.raw('@iif', EL_SIZE, w.size, eps)
+        self.raw('@iif', self.el, w.size, eps)
         for f in ('weight', 'bias', 'running_mean', 'running_var'):
             self.arr(sd[f'{p}.{f}'])
 
     def linear(self, sd, p):
         W = _np(sd[p + '.weight'])
         self.layer('Linear', 'Linear')
-        self.raw('@iii', EL_SIZE, W.shape[0], W.shape[1])
+        self.raw('@iii', self.el, W.shape[0], W.shape[1])
         self.compressed(W)
         self.arr(sd[p + '.bias'])
 
@@ -92,7 +102,7 @@ class _Writer:
         bih, bhh = _np(sd[p + '.bias_ih_l0']), _np(sd[p + '.bias_hh_l0'])
         H = whh.shape[1]
         self.layer('GRU', 'GRU')
-        self.raw('@iii', EL_SIZE, H, wih.shape[1])
+        self.raw('@iii', self.el, H, wih.shape[1])
         for W in (*np.vsplit(wih, 3), *np.vsplit(whh, 3)):
             self.compressed(W)
         for b in (*np.split(bih, 3), *np.split(bhh, 3)):
@@ -103,11 +113,12 @@ class _Writer:
         self.raw('@ii', x, y)
 
 
-def write_bin(f, state_dict, hp, model_type):
-    """Write ``state_dict`` of a ``model_type`` WaveRNN with hparams ``hp`` as a .bin stream."""
+def write_bin(f, state_dict, hp, model_type, el_size=EL_SIZE):
+    """Write ``state_dict`` of a ``model_type`` WaveRNN with hparams ``hp`` as a .bin stream
+    (arrays fp32 for ``el_size`` 4, fp16 for 2)."""
     from .model import MODEL_TYPE_FATCHORD, MODEL_TYPE_GENEING, MODEL_TYPE_RUNTIMERACER
     sd = state_dict
-    w = _Writer(f)
+    w = _Writer(f, el_size)
     scale = int(np.prod(hp.upsample_factors))
     w.raw('@iiii', hp.res_blocks, len(hp.upsample_factors), scale, hp.pad)
     r = 'upsample.resnet'
@@ -125,7 +136,7 @@ def write_bin(f, state_dict, hp, model_type):
         w.stretch(s, 1)
         k = _np(sd[f'upsample.up_layers.{2 * j + 1}.weight']).reshape(-1)
         w.layer('Conv2d', 'Conv2d')
-        w.raw('@ii', EL_SIZE, k.size)
+        w.raw('@ii', w.el, k.size)
         w.arr(k)
     w.linear(sd, 'I')
     if model_type == MODEL_TYPE_FATCHORD:
@@ -142,7 +153,7 @@ def write_bin(f, state_dict, hp, model_type):
         w.linear(sd, fc)
 
 
-def convert_model(model_fpath, default_model_type, out_dir):
+def convert_model(model_fpath, default_model_type, out_dir, el_size=EL_SIZE):
     """convert.py:14-58: checkpoint (``torch.load(weights_only=True)``) -> ``out_dir/<stem>.bin``."""
     import torch
     from .base import hparams_for
@@ -151,7 +162,7 @@ def convert_model(model_fpath, default_model_type, out_dir):
     hp = hparams_for(model_type)
     out = Path(out_dir).joinpath(Path(model_fpath).stem).with_suffix('.bin')
     with open(out, 'wb') as f:
-        write_bin(f, ckpt['model_state'], hp, model_type)
+        write_bin(f, ckpt['model_state'], hp, model_type, el_size)
     return out
 
 
@@ -160,7 +171,10 @@ def config_for(hp, model_type):
     from .model import _MODEL_IDS
     cfg = _abi.WrnnConfig()
     cfg.model_type = _MODEL_IDS[model_type]
-    cfg.mode = _abi.WRNN_MODE_MOL if hp.mode == 'MOL' else _abi.WRNN_MODE_RAW
+    from .model import MODEL_TYPE_GENEING
+    cfg.mode = (_abi.WRNN_MODE_MOL if hp.mode == 'MOL' else
+                _abi.WRNN_MODE_BETA if (model_type == MODEL_TYPE_GENEING and hp.mode == 'RAW') else
+                _abi.WRNN_MODE_RAW)
     cfg.bits = hp.bits
     cfg.rnn_dims, cfg.fc_dims = hp.rnn_dims, hp.fc_dims
     cfg.compute_dims, cfg.res_out_dims = hp.compute_dims, hp.res_out_dims

@@ -47,6 +47,30 @@ def test_bin_loaded_model_equals_state_dict_model(mt, bits, keep):
     assert np.array_equal(a.last_labels, b.last_labels)
 
 
+@pytest.mark.parametrize('mt,bits', [('fatchord-wavernn', 9), ('geneing-wavernn', 10)])
+def test_fp16_bin_model_equals_fp16_rounded_state_dict(mt, bits):
+    """An elSize-2 file runs as the state dict rounded to fp16 (the reader widens exactly)."""
+    from wavernn_amd import convert
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    hp = hparams_for(mt).copy(bits=bits)
+    sd = pruned_state_dict(hp, mt, keep=0.5)
+    sd16 = {k: (v.astype(np.float16).astype(np.float32) if v.dtype == np.float32 else v)
+            for k, v in sd.items()}
+    f = io.BytesIO()
+    convert.write_bin(f, sd, hp, mt, el_size=2)
+    a, b = _model(hp, mt), _model(hp, mt)
+    a.load_state_dict(sd16)
+    b.load_bin(f.getvalue())
+    mel = synth_mel(24, 7) / sp.max_abs_value
+    for m in (a, b):
+        m.set_seed(11)
+        m.generate(mel[None], True, 1000, 100, hp.mu_law, sp.preemphasize,
+                   progress_callback=lambda *x: None)
+    assert np.array_equal(a.last_labels, b.last_labels)
+
+
 def test_libwavernn_vocoder_chunks_match_oracle(tmp_path):
     import torch
     from oracle.wavernn_oracle import oracle_infer_waveform

@@ -52,6 +52,45 @@ def test_bin_round_trip(model_type, bits, keep):
         assert np.array_equal(back[k], v), k
 
 
+@pytest.mark.parametrize('model_type,bits', TOPOLOGIES)
+def test_bin_fp16_round_trip(model_type, bits):
+    """elSize 2 (convert.py:12 'change to 2 for fp16', wavernn.cpp:98): binary16 arrays, widened
+    exactly to fp32 on load -- every tensor equals the state dict rounded to fp16; BatchNorm eps
+    stays fp32. The file is half the size of the fp32 one (plus headers / index streams)."""
+    from wavernn_amd import convert
+    from wavernn_amd.base import hparams_for
+    hp = hparams_for(model_type).copy(bits=bits)
+    sd = pruned_state_dict(hp, model_type, keep=0.5)
+    f16, f32 = io.BytesIO(), io.BytesIO()
+    convert.write_bin(f16, sd, hp, model_type, el_size=2)
+    convert.write_bin(f32, sd, hp, model_type)
+    assert len(f16.getvalue()) < 0.6 * len(f32.getvalue())
+    back = convert.read_bin(f16.getvalue(), hp, model_type)
+    for k, v in sd.items():
+        if k == 'step' or k.endswith('num_batches_tracked'):
+            continue
+        assert np.array_equal(back[k], v.astype(np.float16).astype(np.float32)), k
+    with pytest.raises(ValueError, match='el_size'):
+        convert.write_bin(io.BytesIO(), sd, hp, model_type, el_size=8)
+
+
+def test_half_widening_special_values():
+    """Subnormal, signed zero, inf and the largest half through the reader's widening."""
+    import struct
+    from wavernn_amd import convert
+    from wavernn_amd.base import hparams_for
+    mt = 'geneing-wavernn'
+    hp = hparams_for(mt).copy(bits=9, mode='BITS')
+    sd = pruned_state_dict(hp, mt, keep=1.0)
+    vals = np.array([6e-8, -6e-8, 2.0 ** -14, -0.0, 65504.0, np.inf, -np.inf, 1 / 3], np.float32)
+    sd['upsample.up_layers.1.weight'] = np.resize(vals, sd['upsample.up_layers.1.weight'].shape)
+    f = io.BytesIO()
+    convert.write_bin(f, sd, hp, mt, el_size=2)
+    got = convert.read_bin(f.getvalue(), hp, mt)['upsample.up_layers.1.weight'].reshape(-1)
+    want = np.resize(vals, got.shape).astype(np.float16).astype(np.float32)
+    assert np.array_equal(got, want) and np.signbit(got[3]) and got[0] > 0
+
+
 def test_compress_format():
     """convert.py:60-74 on a hand-made matrix: kept blocks row by row, 255 row ends + 1."""
     from wavernn_amd.convert import compress
@@ -65,6 +104,7 @@ def test_compress_format():
 
 
 def test_bin_errors():
+    import struct
     from wavernn_amd import convert
     from wavernn_amd.base import hparams_for
     mt = 'runtimeracer-wavernn'
@@ -80,6 +120,10 @@ def test_bin_errors():
         convert.read_bin(data, hparams_for(mt).copy(bits=10, mode='RAW'), mt)
     with pytest.raises(ValueError, match='Cannot open file'):
         convert.read_bin(b'\1\2', hp, mt)
+    bad = bytearray(data)
+    bad[16 + 68:16 + 72] = struct.pack('@i', 8)  # elSize of the first layer
+    with pytest.raises(ValueError, match='elSize 8'):
+        convert.read_bin(bytes(bad), hp, mt)
     with pytest.raises(ValueError, match='does not match'):  # fatchord reader, runtimeracer file
         convert.read_bin(data, hparams_for('fatchord-wavernn').copy(bits=9, mode='RAW'),
                          'fatchord-wavernn')
