@@ -189,8 +189,7 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
-    mode = 'BITS' if args.model == 'geneing-wavernn' and args.mode == 'RAW' else args.mode
-    hp = hparams_for(args.model).copy(bits=args.bits, mode=mode)
+    hp = hparams_for(args.model).copy(bits=args.bits, mode=args.mode)  # geneing RAW = Beta
     sd = synth_state_dict(hp, args.model, seed=0)
     model = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
                     hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
@@ -247,7 +246,8 @@ def main():
     total_samples = samples_per_step * args.steps
     value = total_samples / dt
 
-    wname = 'MOL' if mode == 'MOL' else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else '')
+    wname = ('MOL' if hp.mode == 'MOL' else 'RAW (Beta)' if args.model == 'geneing-wavernn' and hp.mode == 'RAW'
+             else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else ''))
     workload = (f'{U}x{args.frames}-frame mel per GPU, {args.model} {wname}, '
                 f'batched folds target={args.target} overlap={args.overlap}')
     roof = None

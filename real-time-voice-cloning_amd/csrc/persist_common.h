@@ -191,7 +191,10 @@ __device__ __forceinline__ void half_argmax(float& v, int& k) {
 // Buffer-resource access: a uniform (SGPR) base and a 32-bit per-lane byte offset, so no
 // 64-bit per-lane addresses stay live across the step loop.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr int kCpNT = 2;  // cache policy: non-temporal (served by L2, bypasses the CU's L1)
+#ifndef WRNN_POLL_CPOL
+#define WRNN_POLL_CPOL 2
+#endif
+constexpr int kCpNT = WRNN_POLL_CPOL;  // cache policy: non-temporal (served by L2, bypasses the CU's L1)
 __device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
