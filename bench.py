@@ -80,9 +80,6 @@ PERSIST_HOPS = {'fatchord-wavernn': 4, 'runtimeracer-wavernn': 8, 'geneing-waver
 
 
 # MACs per row-step of the recurrent weight matrices
-MACS_PER_ROW_STEP = {'fatchord-wavernn': 4071424, 'runtimeracer-wavernn': 2035712}
-
-
 def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False):
     """Lower bound of one persistent step: exchange hops + critical products of one slot.
     Wide launches (kernels_persist_wide.hip) have one more hop (GRU1 is distributed) and run
@@ -270,7 +267,10 @@ def main():
         if name in ('persist', 'persist_wide'):  # one launch per row batch runs all S steps
             roof['us_per_step'] = us / S
             roof['launches_per_generate'] = sum(r[4] for r in info)
-            rows_l = fl / (S * 2.0 * MACS_PER_ROW_STEP.get(args.model, 1)) if S else 0
+            # MACs per row-step as the runtime counts them (weights of I, rnn*, fc*)
+            macs = sum(int(np.prod(v.shape)) for k, v in sd.items()
+                       if k.startswith(('I.', 'rnn', 'fc')) and 'weight' in k)
+            rows_l = fl / (S * 2.0 * macs) if S else 0
             nr = -(-int(round(rows_l)) // 8)
             floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes,
                                            wide=name == 'persist_wide')

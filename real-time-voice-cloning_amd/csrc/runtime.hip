@@ -1914,11 +1914,14 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 11.1 + 0.08 * r});
             }
         } else {
-            for (int r = kPNR; r >= 1; --r)
-                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw)) {
-                    opts.push_back({r, false, 1.0});  // one launch per batch of the largest variant
-                    break;
-                }
+            // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us
+            // at 3 rows, 9.87 at 4; geneing 10-bit 3.91 at 3, 4.56 at 4), linear below; every
+            // spill-free variant is a candidate (18 rows: one launch at 3, not 32 slots at 4)
+            static const double us_rr[kPNR + 1] = {0, 6.7, 7.75, 8.81, 9.87};
+            static const double us_gen[kPNR + 1] = {0, 2.61, 3.26, 3.91, 4.56};
+            for (int r = 1; r <= kPNR; ++r)
+                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw))
+                    opts.push_back({r, false, h->pw.gen ? us_gen[r] : us_rr[r]});
         }
         if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B
             const int c = std::max(1, std::min(kPNR, std::atoi(env)));
