@@ -65,7 +65,7 @@ constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
-template <int NR, bool FC3R>
+template <int NR, bool FC3R, bool MOL>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -88,7 +88,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const bool gate_a = og < 16;        // stage A: W_ih2 (og<16) | W_hh1 (og>=16)
     const int cls = a.cpw * w + og;     // fc3 class of this thread
     const bool has_cls = og < a.cpw && cls < a.n_classes;
-    unsigned* fl = a.flags + (size_t)g * 4 * 64;
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * XB_GROUP);  // this group's exchange area
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
@@ -167,6 +166,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     //   pgn    Gumbel noise of step te, class cls (copied to pgum at the end of step te-1)
     float pP[NR][3], pC[NR];
     float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f, pgn = 0.f;
+    // At <= 16 classes per slot waves 4-7 hold no fc3 class: they issue their GRU1 loads
+    // while waves 0-3 compute fc3 (LDS only) and later poll the candidates; waves 0-3
+    // issue theirs after the candidate publish, off the critical path (a wave polls only
+    // with no bulk loads in flight: its first poll would wait for all of them).
+    constexpr bool EARLY = !FC3R;  // sampling lanes: st = EARLY ? tid - 256 : tid in [0, 32 NR)
     // Loads are unconditional (step indices clamped; past the last step the values go
     // unused): every path to the loop's back edge then consumes them, so the compiler's
     // wait insertion sees no load pending at the top of the step.
@@ -198,8 +202,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pc2 = bld(fcr, o_fc + fo, 2 * H * 4);
                 pf2 = bld(fcr, o_f2 + fo, 0);
             }
-            if (has_cls && a.mode == 0)
+            if (has_cls && !MOL)
                 pgn = bld(mk_rsrc(a.gumbel + (size_t)te * a.B * a.n_classes), o_gum, 0);
+        }
+        // MOL: sampling lane (row r, k < 11) holds draw k of its row (k_mol_noise)
+        if (MOL) {
+            const int sl = EARLY ? tid - 256 : tid;
+            if (sl >= 0 && sl < 32 * NR && (sl & 31) < 11)
+                pgn = bld(mk_rsrc(a.gumbel + ((size_t)te * a.B + g0 + kPG * (sl >> 5)) * kMolNoise),
+                          (unsigned)(sl & 31) * 4u, 0);
         }
     };
     if (tid == 0) lds[L_FAIL] = 0.f;
@@ -434,12 +445,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             prefetch(t, t + 1);  // pgn, not pgum: the fc3 epilogue still reads pgum
         };
 
-        // At <= 16 classes per slot waves 4-7 hold no fc3 class: they issue their GRU1 loads
-        // while waves 0-3 compute fc3 (LDS only) and later poll the candidates; waves 0-3
-        // issue theirs after the candidate publish, off the critical path (a wave polls only
-        // with no bulk loads in flight: its first poll would wait for all of them).
-        constexpr bool EARLY = !FC3R;
-        const int st = EARLY ? tid - 256 : tid;  // sampling lanes: st in [0, 32 NR)
+        const int st = EARLY ? tid - 256 : tid;
         {
             float s0 = 0.f;
             auto fc3 = [&]() {
@@ -485,10 +491,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, lds[L_BCLS + og]);
-                    if (a.mode == 0)
+                    if (!MOL)
                         val = p_add(l, pgum);
-                    else  // MOL: logits row (og == 0 -> wave 0)
-                        bst(l, xr, (unsigned)(kc * 64 + cls) * 4u, (XB_D + XB_D_LOG) * 4);
+                    else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
+                        bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
                 }
                 red[(og * kPNR + kc) * 2] = val;
                 red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             PSTAMP(11);
             if (wv_lo) {
             if (wave == 0) {
-                if (a.mode == 0) {
+                if (!MOL) {
                     // slot candidate per row, tagged with the step (no flag, no wait)
                     const unsigned tag_hi = (seq & kTagSeqMask) << 11;
                     int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
@@ -535,10 +541,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                                     (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
                         }
                     }
-                } else {  // MOL: logits rows + flag
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (tid == 0)
-                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
             if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
@@ -552,10 +554,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         }
         if (FC3R) gru1_loads();
         PSTAMP(7);
-        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, st)) return;
         PSTAMP(8);
         // ================= sample of step t (redundant in every workgroup) ==================
-        if (a.mode == 0) {
+        if (!MOL) {
             if (st >= 0 && st < 32 * NR) {  // half-wave r: lane o polls slot o's candidate of row r
                 const int r = st >> 5, o = st & 31;
                 const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
@@ -595,39 +596,61 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     }
                 }
             }
-        } else if (st >= 0 && st < NR) {
-            // MOL: vocoder/distribution.py:104-140; the Philox draws were turned into
-            // gm_k = log(-log(u1_k)) and lu = log(u2) - log(1 - u2) by k_mol_noise
-            const int r = st, row = g0 + kPG * r;
-            const unsigned lo = (unsigned)(r * 64) * 4u;
+        } else if (st >= 0 && st < 32 * NR) {
+            // MOL: vocoder/distribution.py:104-140. Half-wave r: lane k polls logit k of row r
+            // (tagged pair) and holds draw k of k_mol_noise (gm_k = log(-log(u1_k)), k < 10;
+            // gm_10 = log(u2) - log(1 - u2)), prefetched a step ahead
+            const int r = st >> 5, k = st & 31;
+            const unsigned off = (unsigned)((r * 32 + k) * 2) * 4u;
             const unsigned so = (XB_D + XB_D_LOG) * 4;
-            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
-            float gm[11];
-#pragma unroll
-            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
-            float xv;
-            {
-#pragma clang fp contract(off)
-                float bv = -INFINITY;
-                int bi = 0;
-#pragma unroll
-                for (int k = 0; k < 10; ++k) {
-                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
-                    if (v2 > bv) {
-                        bv = v2;
-                        bi = k;
+            const bool real = k < a.n_classes;
+            const unsigned t0 = p_now();
+            unsigned n = 0;
+            u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+            while (true) {  // two polls in flight (see poll_couples)
+                const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+                if (__all(!real || c.y == seq)) break;
+                c = c1;
+                if ((++n & 255) == 0) {
+                    if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
+                        if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                        lds[L_FAIL] = 1.f;
+                        break;
                     }
                 }
-                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
-                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
-                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
-                ls = ls < lsmin ? lsmin : ls;
-                xv = mean + expf(ls) * gm[10];
-                xv = xv < -1.f ? -1.f : xv;
-                xv = xv > 1.f ? 1.f : xv;
             }
-            lds[L_SX + r] = xv;
-            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+            const float lk = __uint_as_float(c.x);
+            float bv;
+            {
+#pragma clang fp contract(off)
+                bv = k < 10 ? lk - pgum : -INFINITY;
+            }
+            int bi = k < 10 ? k : 0x7fffffff;
+            row16_argmax(bv, bi);  // first max over k < 10 (lanes 0-15 of the half)
+            const int base = (tid & 63) & 32;
+            bi = __shfl(bi, base);
+            bi = bi < 10 ? bi : 0;
+            const float mean = __shfl(lk, base + 10 + bi);
+            float ls = __shfl(lk, base + 20 + bi);
+            const float lu = __shfl(pgum, base + 10);
+            if (k == 0) {
+                float xv;
+                {
+#pragma clang fp contract(off)
+                    const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                    ls = ls < lsmin ? lsmin : ls;
+                    xv = mean + expf(ls) * lu;
+                    xv = xv < -1.f ? -1.f : xv;
+                    xv = xv > 1.f ? 1.f : xv;
+                }
+                lds[L_SX + r] = xv;
+                if (w == 0) {
+                    int rr = r;
+                    asm volatile("" : "+v"(rr));
+                    const int row = g0 + kPG * rr;
+                    bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+                }
+            }
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -764,53 +787,64 @@ size_t persist_flag_words() { return (size_t)kPG * 4 * 64; }
 size_t persist_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
 size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 
-template <int NR, bool FC3R>
+template <int NR, bool FC3R, bool MOL>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
     static bool attr = false;
     const size_t lds = persist_lds_bytes();
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R, MOL>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_persist<NR, FC3R>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    hipLaunchKernelGGL((k_persist<NR, FC3R, MOL>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int NR, bool FC3R>
+template <int NR, bool FC3R, bool MOL>
 int persist_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
-// Scratch bytes of the (rows per group, classes per slot) variant; -1 when it does not exist.
-int persist_variant_scratch(int nr, int cpw) {
+template <int NR>
+int persist_spill_nr(int cpw, int mode) {
+    if (mode != 0) return cpw <= 16 ? persist_spill_t<NR, false, true>() : -1;  // MOL: 30 classes
+    return cpw > 16 ? persist_spill_t<NR, true, false>() : persist_spill_t<NR, false, false>();
+}
+
+// Scratch bytes of the (rows per group, classes per slot, mode) variant; -1 when it does not
+// exist.
+int persist_variant_scratch(int nr, int cpw, int mode) {
     if (cpw < 1 || cpw > kPCls) return -1;
-    const bool r = cpw > 16;
     switch (nr) {
-        case 1: return r ? persist_spill_t<1, true>() : persist_spill_t<1, false>();
-        case 2: return r ? persist_spill_t<2, true>() : persist_spill_t<2, false>();
-        case 3: return r ? persist_spill_t<3, true>() : persist_spill_t<3, false>();
-        case 4: return r ? persist_spill_t<4, true>() : persist_spill_t<4, false>();
+        case 1: return persist_spill_nr<1>(cpw, mode);
+        case 2: return persist_spill_nr<2>(cpw, mode);
+        case 3: return persist_spill_nr<3>(cpw, mode);
+        case 4: return persist_spill_nr<4>(cpw, mode);
         default: return -1;
     }
 }
 
 // 1 when the variant exists and keeps its state in registers (no scratch spills: scratch
 // traffic would serialise behind every exchange).
-int persist_variant_ok(int nr, int cpw) { return persist_variant_scratch(nr, cpw) == 0 ? 1 : 0; }
+int persist_variant_ok(int nr, int cpw, int mode) { return persist_variant_scratch(nr, cpw, mode) == 0 ? 1 : 0; }
+
+template <int NR>
+hipError_t launch_persist_nr(const PersistArgs& a, hipStream_t s) {
+    if (a.mode != 0) return a.cpw <= 16 ? launch_persist_t<NR, false, true>(a, s) : hipErrorInvalidValue;
+    return a.cpw > 16 ? launch_persist_t<NR, true, false>(a, s) : launch_persist_t<NR, false, false>(a, s);
+}
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)
         return hipErrorInvalidValue;
-    const bool r = a.cpw > 16;
     switch (a.nr) {
-        case 1: return r ? launch_persist_t<1, true>(a, s) : launch_persist_t<1, false>(a, s);
-        case 2: return r ? launch_persist_t<2, true>(a, s) : launch_persist_t<2, false>(a, s);
-        case 3: return r ? launch_persist_t<3, true>(a, s) : launch_persist_t<3, false>(a, s);
-        case 4: return r ? launch_persist_t<4, true>(a, s) : launch_persist_t<4, false>(a, s);
+        case 1: return launch_persist_nr<1>(a, s);
+        case 2: return launch_persist_nr<2>(a, s);
+        case 3: return launch_persist_nr<3>(a, s);
+        case 4: return launch_persist_nr<4>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -1900,7 +1900,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
             const int w10 = h->pw.cpw > 16 ? 1 : 0;
             for (int c = 1; c <= kPNR; ++c) {
-                const int sc = persist_variant_scratch(c, h->pw.cpw);
+                const int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode);
                 if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[w10][c]});
             }
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost

@@ -316,8 +316,8 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
                             uint32_t k1, hipStream_t s);
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
                          uint32_t k0, uint32_t k1, hipStream_t s);
-int persist_variant_ok(int nr, int cpw);
-int persist_variant_scratch(int nr, int cpw);
+int persist_variant_ok(int nr, int cpw, int mode);
+int persist_variant_scratch(int nr, int cpw, int mode);
 size_t persist_lds_bytes();
 size_t persist_xbuf_floats();
 size_t persist_flag_words();
