@@ -40,7 +40,7 @@ constexpr int QX_Y = 0;                                  // fc1 hop [GNR][GF] pa
 constexpr int QX_GH = QX_Y + GNR * GF * 2;               // gh1 [GNR][3 GH] pairs
 constexpr int QX_D = QX_GH + GNR * 3 * GH * 2;           // candidates [kPM][GNR] pairs
 constexpr int QX_D_LOG = kPM * GNR * 2;
-constexpr int QX_GROUP = QX_D + QX_D_LOG + GNR * 32 + 64;  // + MOL logits [GNR][32]
+constexpr int QX_GROUP = QX_D + QX_D_LOG + GNR * 64 + 64;  // + MOL / BETA logits [GNR][32] pairs
 
 // LDS carve (floats)
 constexpr int L_XA = 0;                        // [GNR][GH] x1 (fc1 input)
@@ -79,7 +79,8 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
 
 }  // namespace
 
-template <int NR, bool BETA>
+// MODE: 0 RAW (categorical, 'BITS'), 1 MOL, 2 BETA (geneing 'RAW'); each its own instantiation
+template <int NR, int MODE>
 __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -105,7 +106,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
     const bool has_cls = cl < a.cpw && cls < a.n_classes;
     const int j = tid & (GH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
     constexpr int NRH = (NR + 1) / 2;
-    unsigned* fl = a.flags + (size_t)g * 4 * 64;
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * QX_GROUP);
 
     float4 wr[kGNW];
@@ -155,10 +155,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
             if (q == 1 && og < GO)
                 pc = bld(fcr, (unsigned)(p_frame(lri, t, a.hop) * a.cond_width + a.oF1 + o) * 4u, 0);
-            if (has_cls && a.mode == 0)
+            if (has_cls && MODE == 0)
                 pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
                            (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
         }
+        // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
+        if (MODE == 1 && tid < 32 * NR && (tid & 31) < 11)
+            pgum = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + g0 + kPG * (tid >> 5)) * kMolNoise),
+                       (unsigned)(tid & 31) * 4u, 0);
         float pP[NRH][3], pC[NRH];
         {  // (unconditional, step clamped: every path to the back edge consumes these loads)
             const int tn = nxt ? t + 1 : t;
@@ -243,10 +247,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, bcls);
-                    if (a.mode == 0)
-                        val = p_add(l, pgum);
-                    else
-                        bst(l, xr, (unsigned)(kc * 32 + cls) * 4u, (QX_D + QX_D_LOG) * 4);
+                    // (MOL / BETA: the logit itself, published after the gh1 poll below)
+                    val = MODE == 0 ? p_add(l, pgum) : l;
                 }
                 red[(cl * GNR + kc) * 2] = val;
                 red[(cl * GNR + kc) * 2 + 1] = __int_as_float(cls);
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             __syncthreads();
             if (lds[L_FAIL] != 0.f) return;
             if (wave == 0) {
-                if (a.mode == 0) {
+                if (MODE == 0) {
                     const unsigned tag_hi = (seq & kTagSeqMask) << 11;
                     if (a.cpw <= 16) {
                         const int r = tid >> 4, oo = tid & 15;
@@ -289,16 +291,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                                     (unsigned)((w * GNR + r) * 2) * 4u, QX_D * 4, 0);
                         }
                     }
-                } else {  // MOL: logits rows + flag
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (tid == 0)
-                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    // MOL / BETA: the slot's logits (row r, class c) as tagged pairs, polled
+                    // directly by every workgroup's sampling lanes (after this workgroup's gh1
+                    // poll, like the RAW candidates: the gh1 area is single-buffered)
+                    const int r = tid >> 4, c = tid & 15;
+                    if (r < NR && c < a.cpw && a.cpw * w + c < a.n_classes)
+                        bst_tag(red[(c * GNR + r) * 2], seq, xr, (unsigned)(r * 32 + a.cpw * w + c) * 8u,
+                                (QX_D + QX_D_LOG) * 4);
                 }
             }
         }
-        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
         // ================= sample of step t (redundant in every workgroup) ==================
-        if (a.mode == 0) {
+        if (MODE == 0) {
             if (tid < 32 * NR) {
                 const int r = tid >> 5, oo = tid & 31;
                 const unsigned off = (unsigned)((oo * GNR + r) * 2) * 4u;
@@ -335,52 +340,76 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                     }
                 }
             }
-        } else if (BETA) {
-            // BETA (geneing 'RAW'): vocoder/distribution.py:7-20, Beta(exp l0, exp l1) on [-1, 1]
-            // with the Philox gamma draws (philox.h beta_sample), one lane per row
-            if (tid < NR) {
-                const int r = tid, row = g0 + kPG * r;
-                const unsigned lo = (unsigned)(r * 32) * 4u;
-                const unsigned so = (QX_D + QX_D_LOG) * 4;
-                const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[r];
-                const float al = expf(bld_nt(xr, lo, so)), be = expf(bld_nt(xr, lo + 4u, so));
-                const float xv = beta_sample(al, be, (uint32_t)t, (uint32_t)lri.fold, lri.stream,
-                                             a.k0, a.k1);
+        } else if (tid < 32 * NR) {
+            // MOL / BETA: half-wave r, lane k polls logit k of row r (tagged pair)
+            const int r = tid >> 5, k = tid & 31, row = g0 + kPG * r;
+            const unsigned so = (QX_D + QX_D_LOG) * 4;
+            const unsigned off = (unsigned)(r * 32 + k) * 8u;
+            const bool real = k < a.n_classes;
+            const unsigned ts = p_now();
+            unsigned n = 0;
+            u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+            while (true) {  // two polls in flight
+                const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+                if (__all(!real || c.y == seq)) break;
+                c = c1;
+                if ((++n & 255) == 0) {
+                    if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - ts > kSpinTicks) {
+                        if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                        lds[L_FAIL] = 1.f;
+                        break;
+                    }
+                }
+            }
+            const float lk = __uint_as_float(c.x);
+            const int base = (tid & 63) & 32;
+            float xv = 0.f;
+            if (MODE == 2) {
+                // BETA (geneing 'RAW'): vocoder/distribution.py:7-20, Beta(exp l0, exp l1) on
+                // [-1, 1] with the Philox gamma draws (philox.h beta_sample)
+                // [-1, 1] with the Philox gamma draws: lane 0 draws X ~ Gamma(exp l0), lane 1
+                // Y ~ Gamma(exp l1) concurrently (philox.h gamma_mt, g = lane); lane 0 forms
+                // 2 X / (X + Y) - 1 exactly as beta_sample does
+                double gv = 0.0;
+                if (k < 2) {
+                    const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[r];
+                    gv = gamma_mt((double)expf(lk), (uint32_t)k, (uint32_t)t, (uint32_t)lri.fold,
+                                  lri.stream, a.k0, a.k1);
+                }
+                const double gy = __shfl(gv, base + 1);
+                if (k == 0) {
+#pragma clang fp contract(off)
+                    const float sb = (float)(gv / (gv + gy));
+                    xv = 2.0f * sb - 1.0f;
+                }
+            } else {
+                // MOL: vocoder/distribution.py:104-140; lane k holds draw k of k_mol_noise
+                // (gm_k = log(-log(u1_k)), k < 10; gm_10 = log(u2) - log(1 - u2))
+                float bv;
+                {
+#pragma clang fp contract(off)
+                    bv = k < 10 ? lk - pgum : -INFINITY;
+                }
+                int bi = k < 10 ? k : 0x7fffffff;
+                row16_argmax(bv, bi);  // first max over k < 10
+                bi = __shfl(bi, base);
+                bi = bi < 10 ? bi : 0;
+                const float mean = __shfl(lk, base + 10 + bi);
+                float ls = __shfl(lk, base + 20 + bi);
+                const float lu = __shfl(pgum, base + 10);
+                {
+#pragma clang fp contract(off)
+                    const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                    ls = ls < lsmin ? lsmin : ls;
+                    xv = mean + expf(ls) * lu;
+                    xv = xv < -1.f ? -1.f : xv;
+                    xv = xv > 1.f ? 1.f : xv;
+                }
+            }
+            if (k == 0) {
                 lds[L_SX + r] = xv;
                 if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
             }
-        } else if (tid < NR) {
-            // MOL: vocoder/distribution.py:104-140 with the precomputed draws of k_mol_noise
-            const int r = tid, row = g0 + kPG * r;
-            const unsigned lo = (unsigned)(r * 32) * 4u;
-            const unsigned so = (QX_D + QX_D_LOG) * 4;
-            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
-            float gm[11];
-#pragma unroll
-            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
-            float xv;
-            {
-#pragma clang fp contract(off)
-                float bv = -INFINITY;
-                int bi = 0;
-#pragma unroll
-                for (int k = 0; k < 10; ++k) {
-                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
-                    if (v2 > bv) {
-                        bv = v2;
-                        bi = k;
-                    }
-                }
-                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
-                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
-                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
-                ls = ls < lsmin ? lsmin : ls;
-                xv = mean + expf(ls) * gm[10];
-                xv = xv < -1.f ? -1.f : xv;
-                xv = xv > 1.f ? 1.f : xv;
-            }
-            lds[L_SX + r] = xv;
-            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -439,63 +468,65 @@ size_t persist_gen_lds_bytes() {
 }
 size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
 
-// BETA (geneing 'RAW') is its own instantiation: its float64 gamma sampler would otherwise
+// Each sampling mode is its own instantiation: the BETA float64 gamma sampler would otherwise
 // raise the register allocation of the RAW / MOL variants
-template <int NR, bool BETA>
+template <int NR, int MODE>
 hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
     static bool attr = false;
     const size_t lds = persist_gen_lds_bytes();
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR, BETA>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR, MODE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_persist_gen<NR, BETA>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    hipLaunchKernelGGL((k_persist_gen<NR, MODE>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int NR, bool BETA>
+template <int NR, int MODE>
 int persist_gen_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, BETA>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, MODE>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
-template <bool BETA>
+template <int MODE>
 int persist_gen_spill_nr(int nr) {
     switch (nr) {
-        case 1: return persist_gen_spill_t<1, BETA>();
-        case 2: return persist_gen_spill_t<2, BETA>();
-        case 3: return persist_gen_spill_t<3, BETA>();
-        case 4: return persist_gen_spill_t<4, BETA>();
+        case 1: return persist_gen_spill_t<1, MODE>();
+        case 2: return persist_gen_spill_t<2, MODE>();
+        case 3: return persist_gen_spill_t<3, MODE>();
+        case 4: return persist_gen_spill_t<4, MODE>();
         default: return -1;
     }
 }
 
 int persist_gen_variant_ok(int nr, int cpw, int mode) {
-    if (cpw < 1 || cpw > 32) return 0;
+    if (cpw < 1 || cpw > 32 || (mode != 0 && cpw > 16)) return 0;
     // (the BETA variants keep a small stack frame for the float64 trig range reduction)
-    const int sp = mode == 2 ? persist_gen_spill_nr<true>(nr) : persist_gen_spill_nr<false>(nr);
+    const int sp = mode == 2 ? persist_gen_spill_nr<2>(nr)
+                 : mode == 1 ? persist_gen_spill_nr<1>(nr) : persist_gen_spill_nr<0>(nr);
     return sp >= 0 && sp <= (mode == 2 ? 16 : 0) ? 1 : 0;
 }
 
-template <bool BETA>
+template <int MODE>
 hipError_t launch_persist_gen_m(const PersistGenArgs& a, hipStream_t s) {
     switch (a.nr) {
-        case 1: return launch_persist_gen_t<1, BETA>(a, s);
-        case 2: return launch_persist_gen_t<2, BETA>(a, s);
-        case 3: return launch_persist_gen_t<3, BETA>(a, s);
-        case 4: return launch_persist_gen_t<4, BETA>(a, s);
+        case 1: return launch_persist_gen_t<1, MODE>(a, s);
+        case 2: return launch_persist_gen_t<2, MODE>(a, s);
+        case 3: return launch_persist_gen_t<3, MODE>(a, s);
+        case 4: return launch_persist_gen_t<4, MODE>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > 32 ||
-        a.cpw * kPM < a.n_classes || (a.mode != 0 && a.n_classes > 32))
+        a.cpw * kPM < a.n_classes || (a.mode != 0 && (a.n_classes > 32 || a.cpw > 16)))
         return hipErrorInvalidValue;
-    return a.mode == 2 ? launch_persist_gen_m<true>(a, s) : launch_persist_gen_m<false>(a, s);
+    return a.mode == 2 ? launch_persist_gen_m<2>(a, s)
+         : a.mode == 1 ? launch_persist_gen_m<1>(a, s) : launch_persist_gen_m<0>(a, s);
 }
 
 }  // namespace wrnn

@@ -49,7 +49,7 @@ constexpr int RX_GH1 = RX_F + 4 * RX_F_SZ;                 // gh1 [2 parity][kRN
 constexpr int RX_GH1_SZ = kRNR * 4 * RH;
 constexpr int RX_D = RX_GH1 + 2 * RX_GH1_SZ;               // candidates [kPM][kRNR] pairs
 constexpr int RX_D_LOG = kPM * kRNR * 2;
-constexpr int RX_GROUP = RX_D + RX_D_LOG + kRNR * 32 + 64; // + MOL logits [kRNR][32]
+constexpr int RX_GROUP = RX_D + RX_D_LOG + kRNR * 64 + 64; // + MOL logits [kRNR][32] pairs
 
 // LDS carve (floats)
 constexpr int L_XA = 0;                          // [kRNR][RH] stage inputs, ping
@@ -141,7 +141,7 @@ __device__ __forceinline__ bool poll_hop(rsrc_t xr, unsigned so, unsigned seq, f
 
 }  // namespace
 
-template <int NR>
+template <int NR, bool MOL>
 __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -166,7 +166,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     const bool has_cls = cl < a.cpw && cls < a.n_classes;
     const int j = tid & (RH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
     constexpr int NRH = (NR + 1) / 2;
-    unsigned* fl = a.flags + (size_t)g * 4 * 64;
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * RX_GROUP);
 
     // ---- weights -------------------------------------------------------------------------
@@ -393,9 +392,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             }
         }
         float pgum = 0.f;  // Gumbel noise of (row kc, class cls), step t
-        if (own && has_cls && a.mode == 0)
+        if (own && has_cls && !MOL)
             pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
                        (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+        // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
+        if (MOL && tid < 32 * NR && (tid & 31) < 11)
+            pgum = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + g0 + kPG * (tid >> 5)) * kMolNoise),
+                       (unsigned)(tid & 31) * 4u, 0);
         // ================= stage 4: q3 fc1 ==================================================
         if (q == 3) {
             __builtin_amdgcn_s_setprio(2);
@@ -464,17 +467,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, bcls);
-                    if (a.mode == 0)
-                        val = p_add(l, pgum);
-                    else
-                        bst(l, xr, (unsigned)(kc * 32 + cls) * 4u, (RX_D + RX_D_LOG) * 4);
+                    // (MOL: the logit itself, published after the barrier below)
+                    val = MOL ? l : p_add(l, pgum);
                 }
                 red[(cl * kRNR + kc) * 2] = val;
                 red[(cl * kRNR + kc) * 2 + 1] = __int_as_float(cls);
             }
             __syncthreads();
             if (wave == 0) {
-                if (a.mode == 0) {
+                if (!MOL) {
                     const unsigned tag_hi = (seq & kTagSeqMask) << 11;
                     if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
                         const int r = tid >> 4, o = tid & 15;
@@ -506,16 +507,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                                     (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
                         }
                     }
-                } else {  // MOL: logits rows + flag
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (tid == 0)
-                        __hip_atomic_store(fl + 3 * 64 + w, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    // MOL: the slot's logits (row r, class c) as tagged pairs, polled directly
+                    // by every workgroup's sampling lanes
+                    const int r = tid >> 4, c = tid & 15;
+                    if (r < NR && c < a.cpw && a.cpw * w + c < a.n_classes)
+                        bst_tag(red[(c * kRNR + r) * 2], seq, xr, (unsigned)(r * 32 + a.cpw * w + c) * 8u,
+                                (RX_D + RX_D_LOG) * 4);
                 }
             }
         }
-        if (a.mode != 0 && !p_wait(fl + 3 * 64, seq, a.ctl, tid)) return;
         // ================= sample of step t (redundant in every workgroup) ==================
-        if (a.mode == 0) {
+        if (!MOL) {
             if (tid < 32 * NR) {  // half-wave r: lane o polls slot o's tagged candidate of row r
                 const int r = tid >> 5, o = tid & 31;
                 const unsigned off = (unsigned)((o * kRNR + r) * 2) * 4u;
@@ -552,38 +555,56 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                     }
                 }
             }
-        } else if (tid < NR) {
-            // MOL: vocoder/distribution.py:104-140 with the precomputed draws of k_mol_noise
-            const int r = tid, row = g0 + kPG * r;
-            const unsigned lo = (unsigned)(r * 32) * 4u;
+        } else if (tid < 32 * NR) {
+            // MOL: vocoder/distribution.py:104-140. Half-wave r: lane k polls logit k of row r
+            // (tagged pair) and holds draw k of k_mol_noise (gm_k = log(-log(u1_k)), k < 10;
+            // gm_10 = log(u2) - log(1 - u2))
+            const int r = tid >> 5, k = tid & 31, row = g0 + kPG * r;
             const unsigned so = (RX_D + RX_D_LOG) * 4;
-            const rsrc_t nr_ = mk_rsrc(a.gumbel + ((size_t)t * a.B + row) * kMolNoise);
-            float gm[11];
-#pragma unroll
-            for (int k = 0; k < 11; ++k) gm[k] = bld(nr_, 4u * k, 0);
-            float xv;
-            {
-#pragma clang fp contract(off)
-                float bv = -INFINITY;
-                int bi = 0;
-#pragma unroll
-                for (int k = 0; k < 10; ++k) {
-                    const float v2 = bld_nt(xr, lo + 4u * k, so) - gm[k];
-                    if (v2 > bv) {
-                        bv = v2;
-                        bi = k;
+            const unsigned off = (unsigned)(r * 32 + k) * 8u;
+            const bool real = k < a.n_classes;
+            const unsigned ts = p_now();
+            unsigned n = 0;
+            u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+            while (true) {  // two polls in flight
+                const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, so, kCpNT);
+                if (__all(!real || c.y == seq)) break;
+                c = c1;
+                if ((++n & 255) == 0) {
+                    if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - ts > kSpinTicks) {
+                        if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                        lds[L_FAIL] = 1.f;
+                        break;
                     }
                 }
-                const float mean = bld_nt(xr, lo + 4u * (10 + bi), so);
-                float ls = bld_nt(xr, lo + 4u * (20 + bi), so);
-                const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
-                ls = ls < lsmin ? lsmin : ls;
-                xv = mean + expf(ls) * gm[10];
-                xv = xv < -1.f ? -1.f : xv;
-                xv = xv > 1.f ? 1.f : xv;
             }
-            lds[L_SX + r] = xv;
-            if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+            const float lk = __uint_as_float(c.x);
+            const int base = (tid & 63) & 32;
+            float bv;
+            {
+#pragma clang fp contract(off)
+                bv = k < 10 ? lk - pgum : -INFINITY;
+            }
+            int bi = k < 10 ? k : 0x7fffffff;
+            row16_argmax(bv, bi);  // first max over k < 10
+            bi = __shfl(bi, base);
+            bi = bi < 10 ? bi : 0;
+            const float mean = __shfl(lk, base + 10 + bi);
+            float ls = __shfl(lk, base + 20 + bi);
+            const float lu = __shfl(pgum, base + 10);
+            if (k == 0) {
+                float xv;
+                {
+#pragma clang fp contract(off)
+                    const float lsmin = -32.23619130191664f;  // float(np.log(1e-14))
+                    ls = ls < lsmin ? lsmin : ls;
+                    xv = mean + expf(ls) * lu;
+                    xv = xv < -1.f ? -1.f : xv;
+                    xv = xv > 1.f ? 1.f : xv;
+                }
+                lds[L_SX + r] = xv;
+                if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+            }
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -666,51 +687,60 @@ hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s) {
 size_t persist_rr_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
 size_t persist_rr_xbuf_floats() { return (size_t)kPG * RX_GROUP; }
 
-template <int NR>
+template <int NR, bool MOL>
 hipError_t launch_persist_rr_t(const PersistRRArgs& a, hipStream_t s) {
     static bool attr = false;
     const size_t lds = persist_rr_lds_bytes();
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist_rr<NR>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist_rr<NR, MOL>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_persist_rr<NR>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    hipLaunchKernelGGL((k_persist_rr<NR, MOL>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int NR>
+template <int NR, bool MOL>
 int persist_rr_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
-int persist_rr_variant_ok(int nr, int cpw) {
-    if (cpw < 1 || cpw > 32) return 0;
-    int sp = -1;
+template <bool MOL>
+int persist_rr_spill_nr(int nr) {
     switch (nr) {
-        case 1: sp = persist_rr_spill_t<1>(); break;
-        case 2: sp = persist_rr_spill_t<2>(); break;
-        case 3: sp = persist_rr_spill_t<3>(); break;
-        case 4: sp = persist_rr_spill_t<4>(); break;
-        default: break;
+        case 1: return persist_rr_spill_t<1, MOL>();
+        case 2: return persist_rr_spill_t<2, MOL>();
+        case 3: return persist_rr_spill_t<3, MOL>();
+        case 4: return persist_rr_spill_t<4, MOL>();
+        default: return -1;
     }
+}
+
+int persist_rr_variant_ok(int nr, int cpw, int mode) {
+    if (cpw < 1 || cpw > 32 || (mode != 0 && cpw > 16)) return 0;
+    const int sp = mode != 0 ? persist_rr_spill_nr<true>(nr) : persist_rr_spill_nr<false>(nr);
     return sp == 0 ? 1 : 0;
+}
+
+template <bool MOL>
+hipError_t launch_persist_rr_m(const PersistRRArgs& a, hipStream_t s) {
+    switch (a.nr) {
+        case 1: return launch_persist_rr_t<1, MOL>(a, s);
+        case 2: return launch_persist_rr_t<2, MOL>(a, s);
+        case 3: return launch_persist_rr_t<3, MOL>(a, s);
+        case 4: return launch_persist_rr_t<4, MOL>(a, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > 32 ||
-        a.cpw * kPM < a.n_classes || (a.mode != 0 && a.n_classes > 32))
+        a.cpw * kPM < a.n_classes || (a.mode != 0 && (a.n_classes > 32 || a.cpw > 16)))
         return hipErrorInvalidValue;
-    switch (a.nr) {
-        case 1: return launch_persist_rr_t<1>(a, s);
-        case 2: return launch_persist_rr_t<2>(a, s);
-        case 3: return launch_persist_rr_t<3>(a, s);
-        case 4: return launch_persist_rr_t<4>(a, s);
-        default: return hipErrorInvalidValue;
-    }
+    return a.mode != 0 ? launch_persist_rr_m<true>(a, s) : launch_persist_rr_m<false>(a, s);
 }
 
 }  // namespace wrnn

@@ -508,12 +508,21 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
             }
         } else if (a.mode == 2) {
             // BETA (geneing 'RAW'): vocoder/distribution.py:7-20, Beta(exp l0, exp l1) on [-1, 1]
-            if (tid == 0) {
-                const float* lg = a.logits + (size_t)r * n;
-                const float xv = beta_sample(expf(lg[0]), expf(lg[1]), (uint32_t)a.t,
-                                             (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
-                a.samples[(size_t)r * a.S + a.t] = xv;
-                xsh = xv;
+            // lanes 0 / 1 draw the two gammas concurrently (philox.h gamma_mt); lane 0 forms
+            // 2 X / (X + Y) - 1 exactly as beta_sample does
+            if (tid < 64) {
+                double gv = 0.0;
+                if (lane < 2)
+                    gv = gamma_mt((double)expf(a.logits[(size_t)r * n + lane]), (uint32_t)lane,
+                                  (uint32_t)a.t, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+                const double gy = __shfl(gv, 1);
+                if (lane == 0) {
+#pragma clang fp contract(off)
+                    const float sb = (float)(gv / (gv + gy));
+                    const float xv = 2.0f * sb - 1.0f;
+                    a.samples[(size_t)r * a.S + a.t] = xv;
+                    xsh = xv;
+                }
             }
             __syncthreads();
             x = xsh;

@@ -1920,7 +1920,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             static const double us_rr[kPNR + 1] = {0, 6.7, 7.75, 8.81, 9.87};
             static const double us_gen[kPNR + 1] = {0, 2.61, 3.26, 3.91, 4.56};
             for (int r = 1; r <= kPNR; ++r)
-                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw))
+                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw, h->cfg.mode))
                     opts.push_back({r, false, h->pw.gen ? us_gen[r] : us_rr[r]});
         }
         if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B

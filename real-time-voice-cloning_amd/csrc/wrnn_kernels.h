@@ -308,7 +308,7 @@ int persist_gen_variant_ok(int nr, int cpw, int mode);
 size_t persist_gen_lds_bytes();
 size_t persist_gen_xbuf_floats();
 hipError_t launch_persist_rr_init(const PersistRRArgs& a, hipStream_t s);
-int persist_rr_variant_ok(int nr, int cpw);
+int persist_rr_variant_ok(int nr, int cpw, int mode);
 size_t persist_rr_lds_bytes();
 size_t persist_rr_xbuf_floats();
 

@@ -14,12 +14,14 @@ run() {  # run <name> <timeout> cmd...
   if [ $rc -ne 0 ]; then tail -8 "$O/$name.log"; echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 B="python bench.py --steps 3 --warmup 1 --cpu-seconds 0"
-S=${STEPS:-bench,mol,rr9,rr10,gen,beta,c4,c4p,wide,tests,smoke}
+S=${STEPS:-bench,mol,rr9,rr10,rrmol,gen,genmol,beta,c4,c4p,wide,tests,smoke}
 [[ ,$S, == *,bench,* ]] && run bench 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 12
 [[ ,$S, == *,mol,* ]] && run mol 300 $B --mode MOL
 [[ ,$S, == *,rr9,* ]] && run rr9 300 $B --model runtimeracer-wavernn --bits 9
 [[ ,$S, == *,rr10,* ]] && run rr10 300 $B --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000
+[[ ,$S, == *,rrmol,* ]] && run rrmol 300 $B --model runtimeracer-wavernn --mode MOL
 [[ ,$S, == *,gen,* ]] && run gen 300 $B --model geneing-wavernn --mode BITS --bits 10
+[[ ,$S, == *,genmol,* ]] && run genmol 300 $B --model geneing-wavernn --mode MOL
 [[ ,$S, == *,beta,* ]] && run beta 300 $B --model geneing-wavernn --mode RAW
 [[ ,$S, == *,c4,* ]] && run c4 400 $B --utts-per-gpu 8
 # wide launch only (WRNN_PERSIST_WIDE=1): the step-time curve over rows per XCD group
