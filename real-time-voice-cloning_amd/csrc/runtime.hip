@@ -1909,9 +1909,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             const bool scratch_ok = persist_wide_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
             if (wmode && h->pw.wwide && scratch_ok) {
                 if (wmode == 1) opts.clear();
-                // measured: 12.3 us per step at 16 rows per group (the MFMA tiles cost the same
-                // for any row count; the exchanges shrink a little with fewer rows)
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 11.1 + 0.08 * r});
+                // measured per step: 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows per
+                // group (the MFMA tiles cost the same for any row count; the exchanges and
+                // epilogues grow a little with the rows), fit 11.45 + 0.057 r
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 11.45 + 0.057 * r});
             }
         } else {
             // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us
