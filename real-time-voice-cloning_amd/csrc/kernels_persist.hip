@@ -343,6 +343,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path, spread over the
         // exchange waits: rows r % 3 == 0 by waves 0-3 in hop B, r % 3 == 1 by waves 4-7 in hop
         // C, r % 3 == 2 by waves 4-7 in hop D (LDS weights, h2 staged in XH2)
+#ifndef WRNN_HH2_MAP
+#define WRNN_HH2_MAP 0
+#endif
+        // window of row r's gh2: 0 hop B (waves 0-3), 1 hop C (waves 4-7), 2 hop D (waves 4-7)
+        auto hh2_win = [](int r) { return WRNN_HH2_MAP ? (r & 1) : r % 3; };
         auto hh2_rows = [&](auto win_c, int ul) {
             constexpr int WIN = decltype(win_c)::value;
             const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)ul * 3 * kPK4;
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 for (int j = 0; j < 3; ++j) w4[j] = Wh[j * kPK4 + 16 * q + kc];
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    if (r % 3 != WIN) continue;
+                    if (hh2_win(r) != WIN) continue;
                     const float4 x4 = XH2[r * kPK4 + 16 * q + kc];
 #pragma unroll
                     for (int j = 0; j < 3; ++j) dot4(acc[r][j], w4[j], x4);
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                if (r % 3 != WIN) continue;
+                if (hh2_win(r) != WIN) continue;
                 const float t0 = row16_sum(hsum(acc[r][0]));
                 const float t1 = row16_sum(hsum(acc[r][1]));
                 const float t2 = row16_sum(hsum(acc[r][2]));
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     s2 = t2;
                 }
             }
-            if (kc < NR && kc % 3 == WIN) {
+            if (kc < NR && hh2_win(kc) == WIN) {
                 float* gh2 = lds + L_GH2 + ul * 3 * kPNR + kc;
                 const float* b = lds + L_BIAS + 48 + ul;  // b_hh2 of unit 16 w + ul
                 gh2[0] = p_add(s0, b[0]);
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 gru1_loads();
                 XSTAMP(27);
             }
-            } else if (NR > 2) {
+            } else if (NR > 2 && !WRNN_HH2_MAP) {
                 // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
                 hh2_rows(std::integral_constant<int, 2>(), og - 16);
             }
