@@ -181,9 +181,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # WRNN_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a functional rehearsal of the N>1
+    # path on a one-GPU box (its timings mean nothing: the ranks share one GPU)
+    rehearse = os.environ.get('WRNN_BENCH_REHEARSE') == '1'
+    if rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if rehearse:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
     hp = hparams_for(args.model).copy(bits=args.bits, mode=args.mode)  # geneing RAW = Beta
@@ -234,7 +242,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device='cpu' if rehearse else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     samples_per_step = n_utts * (args.frames - 1) * sp.hop_size

@@ -74,6 +74,8 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
     width = max(rows_of)
     dtype = rows.dtype if rows is not None else torch.int16
     dev = device if device is not None else (rows.device if rows is not None else torch.device('cpu'))
+    if dist.get_backend() == 'gloo':  # gloo gathers host tensors (CPU test, 1-GPU rehearsal)
+        dev = torch.device('cpu')
     buf = torch.zeros((width, seq_len), dtype=dtype, device=dev)
     if rows is not None:
         buf[:rows.shape[0]] = rows
