@@ -47,13 +47,14 @@ constexpr int WL_X1 = WL_GH2 + 768;              // x1 of the slot's units [16 n
 constexpr int WL_RI = WL_X1 + 256;               // RowInfo of the group's rows (6 words each)
 constexpr int WL_FAIL = WL_RI + 16 * 6;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
+constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
 constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
 constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
 constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(WL_REG + 4 <= WL_PS, "small LDS arrays overflow their 8 KiB");
+static_assert(WL_BIAS + 112 <= WL_PS, "small LDS arrays overflow their 8 KiB");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -138,6 +139,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
 #define WSTAMP(i) \
     if (trace && t == a.phase_t && (tid & 255) == 0) ph[(tid >> 8) * 12 + (i)] = p_now();
+    // extra stamps of wave 0 at [26, 32): inside the off-path windows
+#define WXSTAMP(i) \
+    if (trace && t == a.phase_t && tid == 0) ph[(i)] = p_now();
 
     // ---- weights ------------------------------------------------------------------------
     float4 wq[4 * kWTiles];  // tile T, k-step ks: wq[4T + ks / 4] component ks % 4
@@ -167,6 +171,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     }
     if (tid < R) reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
     if (tid == 0) lds[WL_FAIL] = 0.f;
+#ifndef WRNN_WIDE_BIAS_LDS
+#define WRNN_WIDE_BIAS_LDS 1
+#endif
+    // biases of the slot in LDS: read per step by the epilogues (a global load there would
+    // hold up the wave's next poll behind its latency)
+    if (tid < 112) {
+        const int k = tid < 96 ? tid % 48 : tid - 96;
+        const float* src = tid < 48 ? a.b_hh1 : tid < 96 ? a.b_hh2 : a.b_fc3;
+        const int idx = tid < 96 ? (k / 16) * kPH + 16 * w + (k & 15) : 16 * w + k;
+        lds[WL_BIAS + tid] = tid >= 96 && 16 * w + k >= a.n_classes ? 0.f : src[idx];
+    }
     // byte offsets: this lane's couple 0 in a hop buffer (consumer); the cell pair's couple
     // (producer: even units publish the pair {u, u + 1})
     const unsigned o_cons = (unsigned)((v * 8 * 64 + l) * 16);
@@ -258,6 +273,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
         {
             fail |= !w_poll8(xr, o_cons, so_h1, seq, bvalid, cc, a.ctl);
+            WXSTAMP(26);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int ks = 0; ks < 16; ++ks) {
@@ -269,6 +285,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             for (int j = 0; j < 3; ++j)
                 *reinterpret_cast<v4f*>(lds + WL_PH + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
         }
+        WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
         fail |= !w_poll8(xr, o_cons, so_x2, seq, bvalid, cc, a.ctl);
         WSTAMP(4);
@@ -305,12 +322,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
                     lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                        p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + j * 16 + ul]
+                                                    : bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
                 }
         }
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
+            WXSTAMP(28);
             fail |= !w_poll8(xr, o_cons, so_h2, seq, bvalid, cc, a.ctl);
+            WXSTAMP(29);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -329,6 +349,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             for (int j = 0; j < 3; ++j)
                 *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
         }
+        WXSTAMP(30);
         // ================= hop B -> stage C: fc2 y1 (critical) =============================
         fail |= !w_poll8(xr, o_cons, so_y1, seq, bvalid, cc, a.ctl);
         WSTAMP(6);
@@ -364,7 +385,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + rn) * 16 + ul];
                     lds[WL_GH2 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, bld(mk_rsrc(a.b_hh2), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                        p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + 48 + j * 16 + ul]
+                                                    : bld(mk_rsrc(a.b_hh2), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
                 }
         }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
@@ -394,7 +416,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     float s = 0.f;
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
-                    val = p_add(p_add(s, bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)), pg);
+                    val = p_add(p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + 96 + cul]
+                                                            : bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)),
+                                pg);
                 }
                 row16_argmax(val, cls);
                 if (cell && cul == 0)
@@ -465,6 +489,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         WSTAMP(11);
     }
 #undef WSTAMP
+#undef WXSTAMP
 #undef WR
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
 }
