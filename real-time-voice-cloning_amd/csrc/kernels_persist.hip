@@ -788,7 +788,6 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
     return hipGetLastError();
 }
 
-size_t persist_flag_words() { return (size_t)kPG * 4 * 64; }
 size_t persist_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
 size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 

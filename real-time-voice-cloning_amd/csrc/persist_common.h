@@ -114,41 +114,6 @@ __device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {
     return rel < ri.L ? ri.fbase + 1 + rel / hop : ri.fbase;
 }
 
-__device__ __forceinline__ bool p_wait(const unsigned* f, unsigned target, unsigned* ctl, int tid) {
-    // the wave of tid 0..63 polls the group's 32 flags (callers pass tid relative to the
-    // polling wave); every wave then meets at the barrier
-    __shared__ int s_fail;
-    if (tid >= 0 && tid < 64) {
-        const unsigned t0 = p_now();
-        unsigned n = 0;
-        bool ok = true;
-        while (true) {
-            const unsigned v = tid < kPM ? ld_nt_u(f + tid) : target;
-            if (__all(v >= target)) break;
-            if ((++n & 255) == 0) {
-                if (ld_sc1_u(ctl + PC_ERR)) {
-                    ok = false;
-                    break;
-                }
-                if (p_now() - t0 > kSpinTicks) {
-                    if (tid == 0) atomicMax(ctl + PC_ERR, 2u);
-                    ok = false;
-                    break;
-                }
-            }
-        }
-        if (tid == 0) s_fail = ok ? 0 : 1;
-    }
-    __syncthreads();
-    return s_fail == 0;
-}
-
-__device__ __forceinline__ void p_publish(unsigned* flag, unsigned value, int tid) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 template <int CTRL>
 __device__ __forceinline__ int pdpp_i(int v) {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);

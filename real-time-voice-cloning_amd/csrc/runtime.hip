@@ -189,7 +189,7 @@ struct wrnn_handle {
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
     } pw;
     struct PersistWS {
-        DevBuf P1, gumbel, ctl, flags, xbuf, st, stamps, phases;
+        DevBuf P1, gumbel, ctl, xbuf, st, stamps, phases;
     } pws;
     int engine = WRNN_ENGINE_AUTO;  // requested engine (wrnn_set_engine / env WRNN_ENGINE)
     int last_engine = WRNN_ENGINE_CHAIN;
@@ -1564,7 +1564,6 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int B = h->last_B, Bp = h->last_Bp, H = kPH, n = h->n_classes;  // H: fatchord layout
     hipStream_t st = h->stream;
     CHECK(P.ctl.alloc(PC_WORDS * sizeof(unsigned)));
-    CHECK(P.flags.alloc(persist_flag_words() * sizeof(unsigned)));
     const bool rr = W.rr, gen = W.gen;
     bool any_wide = false;
     for (const auto& L : h->p_plan) any_wide |= L.wide;
@@ -1584,7 +1583,6 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     }
     PersistArgs a{};
     a.ctl = (unsigned*)P.ctl.p;
-    a.flags = (unsigned*)P.flags.p;
     a.xbuf = P.xbuf.f();
     a.S = S;
     a.B = Bp;
@@ -1629,7 +1627,6 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     PersistRRArgs ar{};
     if (gen) {
         ag.ctl = a.ctl;
-        ag.flags = a.flags;
         ag.xbuf = a.xbuf;
         ag.S = S;
         ag.B = Bp;
@@ -1658,7 +1655,6 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(launch_persist_gen_init(ag, st));
     } else if (rr) {
         ar.ctl = a.ctl;
-        ar.flags = a.flags;
         ar.xbuf = a.xbuf;
         ar.S = S;
         ar.B = Bp;
@@ -1698,7 +1694,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     }
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
     // launches: one per row batch, each running all S steps; the step tags restart with every
-    // batch, so the exchange area and flags are cleared before each. A progress callback does
+    // batch, so the exchange area is cleared before each. A progress callback does
     // not split launches: the kernels publish their step count to a host-mapped word every 100
     // steps (persist_common.h p_progress) and this thread reports from it while they run.
     const int nb = (int)h->p_plan.size();
@@ -1724,7 +1720,6 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.t0 = 0;
         a.t1 = S;
         a.prog_base = b * S;
-        HIPC(hipMemsetAsync(P.flags.p, 0, persist_flag_words() * sizeof(unsigned), st));
         HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
         // registration words only: an error code from an earlier launch stays visible, so the
         // later launches of a failed call exit at registration (p_register)

@@ -171,7 +171,6 @@ constexpr int kProgressEvery = 100;
 
 struct PersistArgs {
     unsigned* ctl;          // PC_WORDS control words
-    unsigned* flags;        // [kPG][4 hops][64]; monotonic step counters within one call
     float* xbuf;            // per-group exchange area (persist_xbuf_floats())
     int t0, t1, S;          // steps [t0, t1) of S
     int B, nr, rb;          // B: row stride of every [t][row] array (padded rows);
@@ -232,7 +231,6 @@ constexpr int kRNW = 28;     // float4 weight registers per thread
 
 struct PersistRRArgs {
     unsigned* ctl;          // PC_WORDS control words
-    unsigned* flags;        // [kPG][4][64] (MOL hop flags)
     float* xbuf;            // per-group exchange area (persist_rr_xbuf_floats())
     int t0, t1, S;
     int B, nr, rb;          // row stride, rows per group, first row of this launch's batch
@@ -276,7 +274,6 @@ constexpr int kGNW = 16;     // float4 weight registers per thread
 
 struct PersistGenArgs {
     unsigned* ctl;
-    unsigned* flags;        // [kPG][4][64] (MOL hop flags)
     float* xbuf;            // per-group exchange area (persist_gen_xbuf_floats())
     int t0, t1, S;
     int B, nr, rb;
@@ -320,6 +317,5 @@ int persist_variant_ok(int nr, int cpw, int mode);
 int persist_variant_scratch(int nr, int cpw, int mode);
 size_t persist_lds_bytes();
 size_t persist_xbuf_floats();
-size_t persist_flag_words();
 
 }  // namespace wrnn
