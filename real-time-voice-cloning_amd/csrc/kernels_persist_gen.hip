@@ -20,6 +20,9 @@
 //            published (so no producer can overwrite them first)
 // then, redundantly in every workgroup, the sample and GRU1 of the next step (rank-1 x term).
 #include "wrnn_kernels.h"
+#ifndef WRNN_POLL_ALL_FIRST
+#define WRNN_POLL_ALL_FIRST 1  // first poll pass loads every couple (measured faster here)
+#endif
 #include "persist_common.h"
 #include "philox.h"
 

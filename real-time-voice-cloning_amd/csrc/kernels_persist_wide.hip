@@ -87,6 +87,23 @@ __device__ __forceinline__ bool w_poll8(rsrc_t xr, unsigned voff, unsigned so, u
     unsigned nsp = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) cc[i] = (u4v){0u, want, 0u, want};
+#ifndef WRNN_WIDE_POLL_ALL_FIRST
+#define WRNN_WIDE_POLL_ALL_FIRST 1
+#endif
+    if (WRNN_WIDE_POLL_ALL_FIRST) {
+        // first pass: all 8 couples in flight at once -- the data is often there already
+        // (one L2 round trip instead of two); then spin on couple 0 as below
+        bool ok = true;
+        if (valid) {
+            unsigned vo = voff;
+            asm volatile("" : "+v"(vo));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ok = ok && cc[i].y == want && cc[i].w == want;
+        }
+        if (__all(ok)) return true;
+    }
     while (true) {
         if (valid) cc[0] = __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, kCpNT);
         if (__all(cc[0].y == want && cc[0].w == want)) {
