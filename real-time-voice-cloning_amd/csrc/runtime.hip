@@ -1693,6 +1693,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(launch_persist_init(a, st));
     }
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
+    if (std::getenv("WRNN_DEBUG_PERSIST_FAIL")) {
+        // test hook: the call's launches find a co-residency error already set at registration
+        // and exit, exercising the real failure path (fallback / error, warning, counters)
+        static const unsigned kInjected = 1u;
+        HIPC(hipMemcpyAsync((unsigned*)P.ctl.p + PC_ERR, &kInjected, sizeof(unsigned), hipMemcpyHostToDevice, st));
+    }
     // launches: one per row batch, each running all S steps; the step tags restart with every
     // batch, so the exchange area is cleared before each. A progress callback does
     // not split launches: the kernels publish their step count to a host-mapped word every 100

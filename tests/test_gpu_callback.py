@@ -5,6 +5,8 @@ when ``i % 100 == 0`` -- so i = 0, 100, ..., in order, once each, b_size = numbe
 On PERSIST the kernels publish their step count to host-mapped memory and the host reports from
 it while one launch per row batch runs all steps (the callback no longer splits launches).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -92,3 +94,41 @@ def test_no_fallback_recorded():
                progress_callback=lambda *a: None)
     assert m.last_engine() == 'persist'
     assert m.fallback_info()[0] == 0
+
+
+@pytest.fixture
+def persist_fails():
+    os.environ['WRNN_DEBUG_PERSIST_FAIL'] = '1'
+    yield
+    os.environ.pop('WRNN_DEBUG_PERSIST_FAIL', None)
+
+
+def test_persist_failure_falls_back_counted_and_warned(persist_fails):
+    """A persistent launch that cannot run (injected co-residency failure at registration):
+    AUTO reruns the call on CHAIN with the same result, counts it, warns, reports 'chain';
+    an explicit 'persist' engine returns the error instead."""
+    meta, gold, m, hp = _model('fatchord_raw9_tiny')
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    with pytest.warns(RuntimeWarning, match='persistent engine could not run'):
+        wav = m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law,
+                         sp.preemphasize, progress_callback=lambda *a: None)
+    assert np.array_equal(wav, gold['wav'])
+    assert m.last_engine() == 'chain'
+    n, why = m.fallback_info()
+    assert n == 1 and 'co-resident' in why
+    m.set_engine('persist')
+    m.set_seed(meta['noise_seed'])
+    with pytest.raises(RuntimeError, match='co-resident'):
+        m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+                   progress_callback=lambda *a: None)
+    # AUTO gives up only after kPersistMaxStreak failed calls in a row: a healthy call
+    # afterwards runs persistent again
+    os.environ.pop('WRNN_DEBUG_PERSIST_FAIL')
+    m.set_engine('auto')
+    m.set_seed(meta['noise_seed'])
+    wav = m.generate(mel[None], True, meta['target'], meta['overlap'], hp.mu_law, sp.preemphasize,
+                     progress_callback=lambda *a: None)
+    assert m.last_engine() == 'persist'
+    assert np.array_equal(wav, gold['wav'])
