@@ -154,8 +154,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * WX_GROUP);
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
-#define WSTAMP(i) \
-    if (trace && t == a.phase_t && (tid & 255) == 0) ph[(tid >> 8) * 12 + (i)] = p_now();
+#define WSTAMP(i)                                                             \
+    if (trace && t == a.phase_t && (tid & 255) == 0) {                        \
+        ph[(tid >> 8) * 12 + (i)] = p_now();                                  \
+        if (tid == 0 && ((i) == 0 || (i) == 10))                              \
+            ph[24 + ((i) == 10)] = (uint32_t)__builtin_amdgcn_s_memtime();    \
+    }
     // extra stamps of wave 0 at [26, 32): inside the off-path windows
 #define WXSTAMP(i) \
     if (trace && t == a.phase_t && tid == 0) ph[(i)] = p_now();
