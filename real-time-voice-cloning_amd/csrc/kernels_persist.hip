@@ -150,7 +150,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
     const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 8u;             // bufA pair (row lr, unit u)
     const unsigned o_y = (unsigned)(lr * kPH + u) * 8u;                 // bufB/C pair (row lr, unit u)
-    const unsigned o_gum = (unsigned)(lrow * a.n_classes + cls) * 4u;   // gumbel row lrow
+    // gumbel row lrow (a padding row reads row rb's: no HBM traffic for padding)
+    const unsigned o_gum = (unsigned)((lrow < a.nreal ? lrow : a.rb) * a.n_classes + cls) * 4u;
     const rsrc_t fcr = mk_rsrc(a.fcond);
     __syncthreads();
 
@@ -177,11 +178,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     auto prefetch = [&](int tg, int te) {
         {  // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
             const int tn = tg + 1 < a.S ? tg + 1 : a.S - 1;
-            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + g0) * 4 * H);
+            const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + a.rb) * 4 * H);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
+                // (a padding row reads row rb's P1: same lines as a real row, no HBM traffic)
+                const int rw = g0 + kPG * r < a.nreal ? g0 - a.rb + kPG * r : 0;
                 const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, o_tid * 4u,
-                                                                     (unsigned)(r * kPG * 4 * H) * 4u, 0);
+                                                                     (unsigned)(rw * 4 * H) * 4u, 0);
                 pP[r][0] = __uint_as_float(v.x);
                 pP[r][1] = __uint_as_float(v.y);
                 pP[r][2] = __uint_as_float(v.z);
@@ -208,8 +211,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // MOL: sampling lane (row r, k < 11) holds draw k of its row (k_mol_noise)
         if (MOL) {
             const int sl = EARLY ? tid - 256 : tid;
+            const int mrow = g0 + kPG * (sl >> 5);
             if (sl >= 0 && sl < 32 * NR && (sl & 31) < 11)
-                pgn = bld(mk_rsrc(a.gumbel + ((size_t)te * a.B + g0 + kPG * (sl >> 5)) * kMolNoise),
+                pgn = bld(mk_rsrc(a.gumbel + ((size_t)te * a.B + (mrow < a.nreal ? mrow : a.rb)) * kMolNoise),
                           (unsigned)(sl & 31) * 4u, 0);
         }
     };

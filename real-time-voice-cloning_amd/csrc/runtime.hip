@@ -1586,6 +1586,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     a.xbuf = P.xbuf.f();
     a.S = S;
     a.B = Bp;
+    a.nreal = B;
     a.nr = Bp / kPG;
     a.mode = h->cfg.mode;
     a.n_classes = n;

@@ -175,6 +175,8 @@ struct PersistArgs {
     int t0, t1, S;          // steps [t0, t1) of S
     int B, nr, rb;          // B: row stride of every [t][row] array (padded rows);
                             // this launch runs rows rb + g + 8 r, r < nr (one row batch)
+    int nreal;              // real rows: rows >= nreal are padding (their stream loads are
+                            // redirected to row rb, so they cost no HBM traffic)
     int mode, n_classes, hop, cpw;  // cpw = classes per workgroup
     const RowInfo* rows;    // [B]
     const float4* wreg;     // [kPM][kPT][persist_reg_f4(cpw)]
