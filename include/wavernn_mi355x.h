@@ -166,6 +166,12 @@ int wrnn_last_engine(wrnn_handle* h, int* engine);
  * warning to stderr; with WRNN_ENGINE_PERSIST requested the call fails instead. AUTO stops
  * trying PERSIST after 3 failed calls in a row. */
 int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_cap);
+/* Launch plan of the last PERSIST call (operator introspection; no reference equivalent):
+ * *n_launches launches; for i < n_launches, launch i runs fold rows first_row[i] + g + 8 r,
+ * r < rows_per_group[i], on the wide MFMA kernel when wide[i] != 0. Arrays may be null;
+ * at most `cap` entries are written. 0 launches after a CHAIN call. */
+int wrnn_plan_info(wrnn_handle* h, int* n_launches, int* first_row, int* rows_per_group, int* wide,
+                   int cap);
 
 /* Per-stage timing of the dominant recurrent kernel. Enable before a call; read after:
  * average duration in microseconds of the launches of stage `stage` in the last call, and

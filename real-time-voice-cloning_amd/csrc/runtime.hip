@@ -2355,6 +2355,20 @@ int wrnn_last_engine(wrnn_handle* h, int* engine) {
     return WRNN_OK;
 }
 
+int wrnn_plan_info(wrnn_handle* h, int* n_launches, int* first_row, int* rows_per_group, int* wide,
+                   int cap) {
+    if (!h || !n_launches) return fail(WRNN_ERR_INVALID, "null argument");
+    const bool p = h->last_engine == WRNN_ENGINE_PERSIST;
+    const int n = p ? (int)h->p_plan.size() : 0;
+    *n_launches = n;
+    for (int i = 0; i < n && i < cap; ++i) {
+        if (first_row) first_row[i] = h->p_plan[i].rb;
+        if (rows_per_group) rows_per_group[i] = h->p_plan[i].nr;
+        if (wide) wide[i] = h->p_plan[i].wide ? 1 : 0;
+    }
+    return WRNN_OK;
+}
+
 int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_cap) {
     if (!h || !count) return fail(WRNN_ERR_INVALID, "null argument");
     *count = h->fallbacks;

@@ -38,7 +38,7 @@ EXPORTED = [
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
-    'wrnn_debug_beta',
+    'wrnn_debug_beta', 'wrnn_plan_info',
 ]
 
 
@@ -122,6 +122,7 @@ def load_library(path=None):
                                        c_void_p, c_int, ctypes.c_double, c_void_p, c_size_t,
                                        c_void_p, c_size_t]),
         'wrnn_debug_noise': (c_int, [c_void_p, c_int, P(ctypes.c_float), c_size_t]),
+        'wrnn_plan_info': (c_int, [c_void_p, P(c_int), P(c_int), P(c_int), P(c_int), c_int]),
         'wrnn_debug_beta': (c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.c_uint32, ctypes.c_float, ctypes.c_float,
                                     P(ctypes.c_float)]),

@@ -191,6 +191,14 @@ class WaveRNN:
         _abi.check(self._lib.wrnn_last_engine(self._h, ctypes.byref(e)))
         return {v: k for k, v in _abi.ENGINES.items()}[e.value]
 
+    def plan_info(self):
+        """Launches of the last persistent call: [(first_row, rows_per_group, wide)]."""
+        n = ctypes.c_int()
+        cap = 64
+        fr, nr, wd = (ctypes.c_int * cap)(), (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+        _abi.check(self._lib.wrnn_plan_info(self._h, ctypes.byref(n), fr, nr, wd, cap))
+        return [(fr[i], nr[i], bool(wd[i])) for i in range(min(n.value, cap))]
+
     def fallback_info(self):
         """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
         n = ctypes.c_int()

@@ -1,0 +1,42 @@
+"""Launch plan of the persistent engine (runtime.hip generate_impl: cost-minimising sequence of
+register-resident and wide launches) on the BASELINE shapes, read back through wrnn_plan_info.
+
+A regression here costs throughput, not correctness, so the parity tests would not notice it:
+in round 2 the runtimeracer / geneing plan took 4 rows per group for 18 rows (one launch,
+padded to 32 slots, 12-17 % slower) until the plan costed every variant."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(model_type, mode, bits, n_utts, frames=1000):
+    import torch
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.model import WaveRNN
+    from wavernn_amd.synth import synth_mel, synth_state_dict
+    hp = hparams_for(model_type).copy(bits=bits, mode=mode)
+    m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
+                hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
+                mode=hp.mode, model_type=model_type, device=0)
+    m.load_state_dict(synth_state_dict(hp, model_type, seed=0))
+    mels = [torch.from_numpy((synth_mel(frames, u) / sp.max_abs_value).astype(np.float32)).cuda()
+            for u in range(n_utts)]
+    m.generate_batch_device(mels, True, 11000, 550)
+    assert m.last_engine() == 'persist'
+    return m.plan_info()
+
+
+@pytest.mark.parametrize('model_type,mode,bits', [('fatchord-wavernn', 'RAW', 9),
+                                                  ('fatchord-wavernn', 'MOL', 9),
+                                                  ('runtimeracer-wavernn', 'RAW', 9),
+                                                  ('geneing-wavernn', 'BITS', 10)])
+def test_c2_shape_is_one_launch_of_3_rows_per_group(model_type, mode, bits):
+    assert _run(model_type, mode, bits, 1) == [(0, 3, False)]
+
+
+def test_c4_shape_is_one_wide_launch_and_one_of_2_rows():
+    plan = _run('fatchord-wavernn', 'RAW', 9, 8)
+    assert sorted((nr, wide) for _, nr, wide in plan) == [(2, False), (16, True)]
+    assert sum(8 * nr for _, nr, _ in plan) == 144
