@@ -126,6 +126,20 @@ def _bounded_leg(args, sd, hp, mel, threads, seconds):
                        f"extrapolated to all steps; {r['t_prepare'] + r['t_loop']:.1f}s measured")
 
 
+def _cpu_share():
+    """CPUs this process may actually use: the cgroup v2 quota (cpu.max) when one is set,
+    else the affinity mask. (The GPU box shows every CPU of the machine in the mask but grants
+    a share of them.)"""
+    n_aff = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if quota != 'max':
+            return max(1, min(n_aff, int(round(int(quota) / int(period))))), 'cgroup cpu.max'
+    except (OSError, ValueError):
+        pass
+    return n_aff, 'affinity mask'
+
+
 def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
     """The oracle (torch-CPU restatement of the reference generate(), pinned bit-exact to the
     reference by tests/test_oracle_golden.py) on this host's cores.
@@ -158,10 +172,17 @@ def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
                  sample=f"whole utterance: {r['B']} folds x {r['S']} steps + upsample + post, "
                         f"{r['t_wall']:.1f}s")]
     legs.append(_bounded_leg(args, sd, hp, mel, 1, args.cpu_seconds / 2))
-    if n_aff > 1 and n_aff != threads:
-        legs.append(_bounded_leg(args, sd, hp, mel, n_aff, args.cpu_seconds / 3))
+    share, share_src = _cpu_share()
+    if share > 1 and share != threads:
+        legs.append(_bounded_leg(args, sd, hp, mel, share, args.cpu_seconds / 3))
+    if n_aff > 1 and n_aff not in (threads, share):
+        # every CPU of the mask: oversubscribes the granted share (reported, not the baseline)
+        leg = _bounded_leg(args, sd, hp, mel, n_aff, args.cpu_seconds / 3)
+        leg['sample'] += f'; {n_aff} threads on a {share}-CPU share ({share_src}): oversubscribed'
+        legs.append(leg)
     torch.set_num_threads(threads)
-    out = dict(legs[0], kind='port', cpu_model=_cpu_model(), affinity_cpus=n_aff, legs=legs)
+    out = dict(legs[0], kind='port', cpu_model=_cpu_model(), affinity_cpus=n_aff,
+               cpu_share=share, cpu_share_source=share_src, legs=legs)
     out['sample'] = (f"oracle.wavernn_oracle (torch-CPU restatement of reference generate()), "
                      f"{args.model} {args.mode} {args.bits}-bit, T={args.frames}, " + legs[0]['sample'])
     return out, parity

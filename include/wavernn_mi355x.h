@@ -217,6 +217,11 @@ int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity);
  * (n_frames, res_out_dims) per utterance 0. */
 int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* aux_out,
                         size_t aux_cap);
+/* Copy the PERSIST conditioning input P1 of the last persistent call for (step, fold row):
+ * 4 * rnn_dims floats, unit-major (r, z, n of W_ih1 (I c) + b_ih1, then I c + b_I) -- the
+ * per-frame form (taps of the upsampler over per-frame projections) the engines consume.
+ * WRNN_ERR_INVALID when the last call did not run the persistent engine. */
+int wrnn_debug_p1(wrnn_handle* h, int step, int row, float* out, size_t capacity);
 
 #ifdef __cplusplus
 }

@@ -264,4 +264,70 @@ hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, f
     return hipGetLastError();
 }
 
+// Per-frame P1 expansion (launch_p1_expand, wrnn_kernels.h). A thread owns one float4 column
+// chunk of one fold row over a run of kP1Run consecutive steps: the five frame projections
+// around the current frame and its aux term stay in registers while the run stays inside one
+// frame (hop steps), so an output float4 costs one store and ~6 / kP1Run loads. The phase taps
+// are uniform over the workgroup (scalar loads). Output: one coalesced 1-KiB store per wave.
+constexpr int kP1Run = 64;
+__global__ __launch_bounds__(kThreads) void k_p1_expand(float4* __restrict__ P1, int Btot,
+                                                        int row0, int S, int tpo, int L, int hop,
+                                                        int T, int nq, const float4* __restrict__ q,
+                                                        const float4* __restrict__ a,
+                                                        const float* __restrict__ taps) {
+    const int c = blockIdx.x * kThreads + threadIdx.x;
+    const int fo = blockIdx.y, t0 = blockIdx.z * kP1Run;
+    if (c >= nq) return;
+    const int t1 = t0 + kP1Run < S ? t0 + kP1Run : S;
+    const float4 z4 = {0.f, 0.f, 0.f, 0.f};
+    float4 r[5], av = z4;
+    int fc = -2;  // frame of the operands in registers (-1: the zero tail pad)
+    for (int t = t0; t < t1; ++t) {
+        const int p = fo * tpo + t;  // fold_with_overlap position
+        const int f = p < L ? p / hop : -1;
+        if (f != fc) {
+            fc = f;
+            if (f < 0) {
+                av = a[c];  // zero frame: bias only
+            } else {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const int j = f - 2 + k;
+                    r[k] = (j >= 0 && j < T) ? q[(size_t)(j + 1) * nq + c] : z4;
+                }
+                av = a[(size_t)(f + 1) * nq + c];
+            }
+        }
+        float4 v = av;
+        if (f >= 0) {
+            const float* K = taps + (size_t)(p - f * hop) * 8;
+            float4 m = z4;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                m.x = fmaf(K[k], r[k].x, m.x);
+                m.y = fmaf(K[k], r[k].y, m.y);
+                m.z = fmaf(K[k], r[k].z, m.z);
+                m.w = fmaf(K[k], r[k].w, m.w);
+            }
+            v.x = m.x + av.x;
+            v.y = m.y + av.y;
+            v.z = m.z + av.z;
+            v.w = m.w + av.w;
+        }
+        P1[((size_t)t * Btot + row0 + fo) * nq + c] = v;
+    }
+}
+
+hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int S, int tpo, int L, int hop,
+                            int T, int nq, const float* q, const float* a, const float* taps,
+                            hipStream_t s) {
+    if (Bu <= 0 || S <= 0 || nq <= 0) return hipSuccess;
+    if (hop <= 0 || T <= 0 || Bu > 65535) return hipErrorInvalidValue;
+    dim3 grid((nq + kThreads - 1) / kThreads, Bu, (S + kP1Run - 1) / kP1Run);
+    hipLaunchKernelGGL(k_p1_expand, grid, dim3(kThreads), 0, s, reinterpret_cast<float4*>(P1), Btot,
+                       row0, S, tpo, L, hop, T, nq, reinterpret_cast<const float4*>(q),
+                       reinterpret_cast<const float4*>(a), taps);
+    return hipGetLastError();
+}
+
 }  // namespace wrnn

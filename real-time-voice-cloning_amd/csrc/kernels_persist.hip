@@ -44,7 +44,9 @@ constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][v
 constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
 constexpr int XB_G = XB_D + XB_D_SZ;              // gh1 [parity][r][unit] (r, z, n, -) float4
 constexpr int XB_G_SZ = 2 * kPNR * kPH * 4;
-constexpr int XB_GROUP = XB_G + XB_G_SZ + 64;
+constexpr int XB_P = XB_G + XB_G_SZ;              // P1 ring [parity][r][unit] (r, z, n, cI) float4
+constexpr int XB_P_SZ = 2 * kPNR * kPH * 4;
+constexpr int XB_GROUP = XB_P + XB_P_SZ + 64;
 
 // LDS carve (floats). The per-step operands come first so every ds_read offset of the inner
 // loops fits the 16-bit immediate (no per-(q, row) address registers).
@@ -65,7 +67,8 @@ constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
-template <int NR, bool FC3R, bool MOL>
+// P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
+template <int NR, bool FC3R, bool MOL, bool P1R>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -175,8 +178,51 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // Loads are unconditional (step indices clamped; past the last step the values go
     // unused): every path to the loop's back edge then consumes them, so the compiler's
     // wait insertion sees no load pending at the top of the step.
+    // P1R producer lanes: waves 4-7 (og >= 16), lane kc < 4 NR forms component kc % 4 of P1
+    // (row kc / 4, unit u) of step t + 2 from the per-frame projections: the taps of its phase
+    // and the five frame rows around its frame, loaded with the step's GRU1 operands
+    const bool p1own = P1R && !gate_a && kc < 4 * NR;
+    float pk = 0.f, pq[4], pa = 0.f;  // pk: tap (kc % 4) of the phase, quad-broadcast at use
+    auto p1_loads = [&](int tau) {  // operands of P1(tau) for this producer lane
+        if (!p1own) return;
+        int tx = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
+        asm volatile("" : "+v"(tx));
+        const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15);
+        const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kx >> 2];
+        tau = tau < a.S ? tau : a.S - 1;
+        const unsigned p = (unsigned)(ri.rel0 + tau);
+        const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
+        const unsigned f = p / (unsigned)a.hop, sph = in ? p - f * (unsigned)a.hop : 0u;
+        // frame slots (runtime.hip): zero frame at fbase, frame j at fbase + 1 + j, zero guard
+        // slots at fbase - 1 and fbase + T + 1, + 2: the phase's 4 frames need no bounds check
+        const unsigned s0 = in ? (unsigned)ri.fbase - 1u + f + (sph >= (unsigned)a.p1split ? 1u : 0u)
+                               : (unsigned)ri.fbase;
+        const unsigned col = (unsigned)(4 * ux + (kx & 3)) * 4u;
+        // the 4 lanes of a row (one DPP quad) load its 4 taps, one each
+        pk = bld(mk_rsrc(a.p1taps), (sph * 4u + (unsigned)(kx & 3)) * 4u, 0);
+        const rsrc_t qr = mk_rsrc(a.p1q);
+        constexpr unsigned kRow = 4u * kPH * 4u;  // bytes per frame slot
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pq[k] = bld(qr, (in ? s0 + (unsigned)k : s0) * kRow + col, 0);
+        pa = bld(mk_rsrc(a.p1a), (in ? (unsigned)ri.fbase + 1u + f : s0) * kRow + col, 0);
+    };
+    // P1(tau) into ring slot tau & 1: k_p1_expand's fma chain without its zero taps, so the
+    // same values as the stream
+    auto p1_store = [&](int tau) {
+        if (!p1own) return;
+        float m = 0.f;  // tap k from quad lane k (quad_perm(k, k, k, k))
+        m = fmaf(pdpp<0x00>(pk), pq[0], m);
+        m = fmaf(pdpp<0x55>(pk), pq[1], m);
+        m = fmaf(pdpp<0xAA>(pk), pq[2], m);
+        m = fmaf(pdpp<0xFF>(pk), pq[3], m);
+        int tx = tid;
+        asm volatile("" : "+v"(tx));
+        const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15);
+        const unsigned o = (unsigned)((((tau & 1) * kPNR + (kx >> 2)) * kPH + ux) * 4 + (kx & 3)) * 4u;
+        bst(p_add(m, pa), xr, o, XB_P * 4);
+    };
     auto prefetch = [&](int tg, int te) {
-        {  // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
+        if constexpr (!P1R) {  // P1 is [step][row][unit][r, z, n, cI]: one 16-byte load per row
             const int tn = tg + 1 < a.S ? tg + 1 : a.S - 1;
             const rsrc_t pr = mk_rsrc(a.P1 + ((size_t)tn * a.B + a.rb) * 4 * H);
 #pragma unroll
@@ -218,6 +264,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         }
     };
     if (tid == 0) lds[L_FAIL] = 0.f;
+    if constexpr (P1R) {  // ring prologue: P1(t0 + 1), read by GRU1 of step t0
+        __syncthreads();  // RowInfo in LDS
+        p1_loads(a.t0 + 1);
+        p1_store(a.t0 + 1);
+    }
     prefetch(a.t0, a.t0);
     pgum = pgn;
     __syncthreads();
@@ -420,6 +471,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         if (gate_a) {
             const float y = mv1(pf2);
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_C * 4);
+        } else {
+            // P1 ring: operands of P1(t + 2), issued while no poll is in flight on this CU
+            // (fc2 is LDS + VALU on waves 0-3); stored in hop C
+            p1_loads(t + 2);
         }
         PSTAMP(5);
         __syncthreads();  // fc2 has read X0: y2 may be staged over it
@@ -434,7 +489,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
             if (!poll_couples<NR>(xr, off, XB_C * 4, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         } else {
+            // P1 ring: P1(t + 2) (operands loaded in stage C) into slot t & 1 (P1(t) there was
+            // read at step t - 1: every slot is past it)
             if (NR > 1) hh2_rows(std::integral_constant<int, 1>(), og - 16);
+            p1_store(t + 2);
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -451,6 +509,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pG[r][1] = __uint_as_float(v.y);
                 pG[r][2] = __uint_as_float(v.z);
             }
+            if constexpr (P1R)  // P1(t + 1) from the ring (stored at step t - 1 / the prologue,
+                                // ordered before this step's y1 as gh1 is)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
+                        xr, o_tid * 4u, (unsigned)(XB_P + (((t + 1) & 1) * kPNR + r) * kPH * 4) * 4u, kCpNT);
+                    pP[r][0] = __uint_as_float(v.x);
+                    pP[r][1] = __uint_as_float(v.y);
+                    pP[r][2] = __uint_as_float(v.z);
+                    pC[r] = __uint_as_float(v.w);
+                }
             prefetch(t, t + 1);  // pgn, not pgum: the fc3 epilogue still reads pgum
         };
 
@@ -556,9 +625,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 gru1_loads();
                 XSTAMP(27);
             }
-            } else if (NR > 2 && !WRNN_HH2_MAP) {
+            } else {
                 // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
-                hh2_rows(std::integral_constant<int, 2>(), og - 16);
+                if (NR > 2 && !WRNN_HH2_MAP) hh2_rows(std::integral_constant<int, 2>(), og - 16);
             }
         }
         if (FC3R) gru1_loads();
@@ -795,64 +864,76 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
 size_t persist_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
 size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 
-template <int NR, bool FC3R, bool MOL>
+template <int NR, bool FC3R, bool MOL, bool P1R>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
     static bool attr = false;
     const size_t lds = persist_lds_bytes();
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R, MOL>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R, MOL, P1R>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_persist<NR, FC3R, MOL>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    hipLaunchKernelGGL((k_persist<NR, FC3R, MOL, P1R>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }
 
-template <int NR, bool FC3R, bool MOL>
+template <int NR, bool FC3R, bool MOL, bool P1R>
 int persist_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
-template <int NR>
+template <int NR, bool P1R>
 int persist_spill_nr(int cpw, int mode) {
-    if (mode != 0) return cpw <= 16 ? persist_spill_t<NR, false, true>() : -1;  // MOL: 30 classes
-    return cpw > 16 ? persist_spill_t<NR, true, false>() : persist_spill_t<NR, false, false>();
+    if (mode != 0) return cpw <= 16 ? persist_spill_t<NR, false, true, P1R>() : -1;  // MOL: 30 classes
+    return cpw > 16 ? persist_spill_t<NR, true, false, P1R>() : persist_spill_t<NR, false, false, P1R>();
 }
 
-// Scratch bytes of the (rows per group, classes per slot, mode) variant; -1 when it does not
-// exist.
-int persist_variant_scratch(int nr, int cpw, int mode) {
+// Scratch bytes of the (rows per group, classes per slot, mode, P1 ring) variant; -1 when it
+// does not exist.
+int persist_variant_scratch(int nr, int cpw, int mode, int ring) {
     if (cpw < 1 || cpw > kPCls) return -1;
-    switch (nr) {
-        case 1: return persist_spill_nr<1>(cpw, mode);
-        case 2: return persist_spill_nr<2>(cpw, mode);
-        case 3: return persist_spill_nr<3>(cpw, mode);
-        case 4: return persist_spill_nr<4>(cpw, mode);
+    switch (nr * 2 + (ring ? 1 : 0)) {
+        case 2: return persist_spill_nr<1, false>(cpw, mode);
+        case 3: return persist_spill_nr<1, true>(cpw, mode);
+        case 4: return persist_spill_nr<2, false>(cpw, mode);
+        case 5: return persist_spill_nr<2, true>(cpw, mode);
+        case 6: return persist_spill_nr<3, false>(cpw, mode);
+        case 7: return persist_spill_nr<3, true>(cpw, mode);
+        case 8: return persist_spill_nr<4, false>(cpw, mode);
+        case 9: return persist_spill_nr<4, true>(cpw, mode);
         default: return -1;
     }
 }
 
 // 1 when the variant exists and keeps its state in registers (no scratch spills: scratch
 // traffic would serialise behind every exchange).
-int persist_variant_ok(int nr, int cpw, int mode) { return persist_variant_scratch(nr, cpw, mode) == 0 ? 1 : 0; }
+int persist_variant_ok(int nr, int cpw, int mode, int ring) {
+    return persist_variant_scratch(nr, cpw, mode, ring) == 0 ? 1 : 0;
+}
 
-template <int NR>
+template <int NR, bool P1R>
 hipError_t launch_persist_nr(const PersistArgs& a, hipStream_t s) {
-    if (a.mode != 0) return a.cpw <= 16 ? launch_persist_t<NR, false, true>(a, s) : hipErrorInvalidValue;
-    return a.cpw > 16 ? launch_persist_t<NR, true, false>(a, s) : launch_persist_t<NR, false, false>(a, s);
+    if (a.mode != 0) return a.cpw <= 16 ? launch_persist_t<NR, false, true, P1R>(a, s) : hipErrorInvalidValue;
+    return a.cpw > 16 ? launch_persist_t<NR, true, false, P1R>(a, s) : launch_persist_t<NR, false, false, P1R>(a, s);
 }
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.rb + kPG * a.nr > a.B || a.cpw < 1 || a.cpw > kPCls || a.cpw * kPM < a.n_classes)
         return hipErrorInvalidValue;
-    switch (a.nr) {
-        case 1: return launch_persist_nr<1>(a, s);
-        case 2: return launch_persist_nr<2>(a, s);
-        case 3: return launch_persist_nr<3>(a, s);
-        case 4: return launch_persist_nr<4>(a, s);
+    const bool ring = a.p1q != nullptr;
+    if (ring && (!a.p1a || !a.p1taps || a.hop <= 0)) return hipErrorInvalidValue;
+    switch (a.nr * 2 + (ring ? 1 : 0)) {
+        case 2: return launch_persist_nr<1, false>(a, s);
+        case 3: return launch_persist_nr<1, true>(a, s);
+        case 4: return launch_persist_nr<2, false>(a, s);
+        case 5: return launch_persist_nr<2, true>(a, s);
+        case 6: return launch_persist_nr<3, false>(a, s);
+        case 7: return launch_persist_nr<3, true>(a, s);
+        case 8: return launch_persist_nr<4, false>(a, s);
+        case 9: return launch_persist_nr<4, true>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

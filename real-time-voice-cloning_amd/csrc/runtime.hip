@@ -158,6 +158,7 @@ struct wrnn_handle {
         DevBuf slots[SL_COUNT];
         DevBuf labels, samples, noise, cI, fcond, rows, stamps;
         DevBuf mel_in, act0, act1, Rb, up1, up2, melup;
+        DevBuf q4, a4;  // per-frame P1 projections [1 + T][np] (slot 0 = zero frame)
         size_t mel_in_cap = 0;
     } ws;
     // captured recurrence chunks: (t0, len, S if last chunk else -1, rows, timing, MOL seed)
@@ -165,6 +166,9 @@ struct wrnn_handle {
 
     // ---- call state
     int last_B = 0, last_S = 0, last_L0 = 0, last_T0 = 0;
+    bool melup_valid = false;  // ws.melup holds the last call's upsampled mel (not per-frame P1)
+    bool p1_ring = false;      // this call's k_persist launches form P1 in-kernel
+    bool p1_stream = false;    // this call writes the [S][B][4H] P1 stream (other kernels)
     bool timing = false;
     int phase_step = -1;  // diagnostic (env WRNN_PHASE_STEP): per-phase stamps of one step
     DevBuf phases;
@@ -183,6 +187,10 @@ struct wrnn_handle {
         const float *wreg = nullptr, *wlds = nullptr;
         const float *M1T = nullptr, *bP1 = nullptr;  // P1 straight from the conditioning input
         bool p1x4 = false;  // fatchord: P1 as [step][row][unit][r, z, n, cI] (one 16-B load)
+        // P1 from per-frame projections + the upsampler's per-phase taps (pack_p1)
+        bool p1taps_ok = false;
+        const float *p1taps = nullptr, *zero_np = nullptr;
+        int p1split = -1;  // phase from which the 4 in-kernel taps start at frame f - 1
         const float *wwide = nullptr, *wwide_lds = nullptr;  // wide-row launches (MFMA images)
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
@@ -427,6 +435,93 @@ int pack_p1(wrnn_handle* h, bool x4) {
         CHECK(rc);
         P.bP1 = upload(h, bP1, &rc);
         CHECK(rc);
+        P.zero_np = upload(h, std::vector<float>(bP1.size(), 0.f), &rc);
+        CHECK(rc);
+    }
+    // Per-frame form of P1 (persistent engines): the mel upsampler (fatchord_version.py:47-85)
+    // is linear, and for every real frame its response is the same kernel shifted by hop (the
+    // `pad` zero frames keep it clear of the sequence ends), so
+    //   mel_up(hop f + s) = sum_k K[s][k] mel(f - 2 + k),  k < 5,
+    //   P1(p) = M1 [mel_up(p); aux(f)] + bP1 = sum_k K[s][k] Q(f - 2 + k) + Aq(f),
+    // Q = M1_mel mel and Aq = M1_aux aux + bP1 per FRAME (two K = 80 / 31 GEMMs over T frames)
+    // instead of one K = 111 GEMM per (step, row) over the upsampled mel. K comes from the
+    // reference's own stencil chain run on unit impulses in float64 and is checked on every
+    // frame of a test sequence; a chain that does not have this form keeps the GEMM path.
+    P.p1taps_ok = false;
+    {
+        const int nu = h->cfg.n_upsample, pad = h->cfg.pad, hop = h->hop, Tt = 9;
+        std::vector<std::vector<double>> resp(Tt);
+        bool ok = nu >= 1 && hop > 0;
+        for (int j = 0; j < Tt && ok; ++j) {
+            std::vector<double> cur(Tt, 0.0);
+            cur[j] = 1.0;
+            int in_pad = pad, T_in = Tt, W_in = Tt + 2 * pad;
+            for (int st = 0; st < nu; ++st) {  // k_mel_stencil in float64
+                const int s = h->cfg.upsample_factors[st];
+                const auto it = T.find("upsample.up_layers." + std::to_string(2 * st + 1) + ".weight");
+                if (it == T.end() || (int)it->second.size() != 2 * s + 1) {
+                    ok = false;
+                    break;
+                }
+                const auto& wk = it->second;
+                const int W_out = W_in * s;
+                const bool last = st == nu - 1;
+                const int lo = last ? h->indent : 0, len = last ? W_out - 2 * h->indent : W_out;
+                std::vector<double> out(len > 0 ? len : 0, 0.0);
+                for (int oo = 0; oo < len; ++oo)
+                    for (int d = 0; d <= 2 * s; ++d) {
+                        const int i = lo + oo + d - s;
+                        const int q = (i >= 0 && i < W_out) ? i / s - in_pad : -1;
+                        if (q >= 0 && q < T_in) out[oo] += (double)wk[d] * cur[q];
+                    }
+                cur.swap(out);
+                in_pad = 0;
+                T_in = W_in = len;
+            }
+            if ((int)cur.size() != hop * Tt) ok = false;
+            resp[j] = std::move(cur);
+        }
+        // kernel G(x) = response of frame jm at hop jm + x; taps must lie in frames f-2 .. f+2
+        std::vector<float> taps((size_t)hop * 8, 0.f);
+        if (ok) {
+            const int jm = Tt / 2;
+            auto G = [&](int x) {
+                const int p = hop * jm + x;
+                return (p >= 0 && p < hop * Tt) ? resp[jm][p] : 0.0;
+            };
+            for (int p = 0; p < hop * Tt && ok; ++p) {  // support inside [-2 hop, 3 hop)
+                const int x = p - hop * jm;
+                if (G(x) != 0.0 && (x < -2 * hop || x >= 3 * hop)) ok = false;
+            }
+            for (int j = 0; j < Tt && ok; ++j)  // shift invariance on every frame, edges included
+                for (int p = 0; p < hop * Tt && ok; ++p) {
+                    const double a = resp[j][p], b = G(p - hop * j);
+                    if (std::fabs(a - b) > 1e-12 * (1.0 + std::fabs(b))) ok = false;
+                }
+            // mel_up(hop f + s) = sum_e G(s + hop e) mel(f - e); k = 2 - e
+            for (int s = 0; s < hop && ok; ++s)
+                for (int k = 0; k < 5; ++k) taps[(size_t)s * 8 + k] = (float)G(s + hop * (2 - k));
+        }
+        // the in-kernel form (k_persist P1 ring) reads 4 taps: k0 .. k0 + 3 with k0 = 0 below
+        // phase `split` and 1 from it on (tap 4 is zero below, tap 0 zero from it on); the
+        // sums are the same fma chains, zero taps adding nothing
+        int split = -1;
+        for (int c = 0; c <= hop && ok && split < 0; ++c) {
+            bool good = true;
+            for (int s = 0; s < hop && good; ++s)
+                good = taps[(size_t)s * 8 + (s < c ? 4 : 0)] == 0.f;
+            if (good) split = c;
+        }
+        if (ok) {
+            std::vector<float> all = taps;  // [hop][8] then [hop][4]
+            all.resize((size_t)hop * 12, 0.f);
+            for (int s = 0; split >= 0 && s < hop; ++s)
+                for (int i = 0; i < 4; ++i) all[(size_t)hop * 8 + s * 4 + i] = taps[(size_t)s * 8 + (s >= split) + i];
+            P.p1taps = upload(h, all, &rc);
+            CHECK(rc);
+            P.p1taps_ok = true;
+            P.p1split = split;  // -1: no 4-tap form, the stream is used
+        }
     }
     return WRNN_OK;
 }
@@ -1007,6 +1102,25 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
     return WRNN_OK;
 }
 
+// Per-frame P1 (pack_p1) unless WRNN_P1_FRAMES=0 (A/B against the per-(step, row) GEMM).
+static bool p1_frames_enabled() {
+    static const bool on = [] {
+        const char* env = std::getenv("WRNN_P1_FRAMES");
+        return !(env && std::atoi(env) == 0);
+    }();
+    return on;
+}
+
+// The fatchord register-resident kernel can form P1 in-kernel (per-frame form available).
+// WRNN_P1_RING=0 (read per call) keeps the stream for every kernel (A/B, tests: the ring and
+// the stream carry bit-identical values).
+static bool p1_ring_ok(const wrnn_handle* h) {
+    const char* env = std::getenv("WRNN_P1_RING");
+    if (env && std::atoi(env) == 0) return false;
+    return !h->pw.rr && !h->pw.gen && h->pw.p1x4 && h->pw.p1taps_ok && h->pw.p1split >= 0 &&
+           p1_frames_enabled();
+}
+
 // ---- upsample network + conditioning for one utterance --------------------------------
 int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
                  int row0, int fbase, float* P1out) {
@@ -1088,8 +1202,11 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         e3.bias = h->bco;
         HIPC(launch_gemm(R, T, C, a3, b3, e3, st));
     }
+    // PERSIST with the per-frame P1 (pack_p1): no upsampled mel is needed at all
+    const bool p1f = P1out && h->pw.p1x4 && h->pw.p1taps_ok && p1_frames_enabled();
+    h->melup_valid = !p1f;
     // mel stretch+conv stencils (fatchord_version.py:68-76,83-84)
-    {
+    if (!p1f) {
         const int nu = h->cfg.n_upsample;
         const float* src = d_mel;
         int in_pad = h->cfg.pad, T_in = T, W_in = T + 2 * h->cfg.pad;
@@ -1140,7 +1257,36 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         e4.row0 = row0;
         // the x4 P1 carries cI as its fourth column: the persistent kernels never read ws.cI
         if (!(P1out && h->pw.p1x4)) HIPC(launch_gemm(S * Bu, H, h->KI, a4, b4, e4, st));
-        if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
+        if (p1f) {  // PERSIST, per-frame form: Q = M1_mel mel, Aq = M1_aux aux + bP1, then taps
+            const int np = 4 * H;  // frame slots [fbase, fbase + T] of this utterance
+            if ((size_t)(fbase + T + 3) * np * sizeof(float) > ws.q4.bytes || fbase < 1)
+                return fail(WRNN_ERR_INVALID, "frame slots exceed the workspace");
+            GemmA aq{};
+            GemmB bq{};
+            GemmEp eq{};
+            aq.kind = 2;  // frame-A: slot 0 = zero frame, slot j + 1 = frame j
+            aq.R = d_mel;
+            aq.ldr = T;
+            aq.r_off = 0;
+            bq.kind = 0;
+            bq.p = h->pw.M1T;
+            bq.ld = np;
+            eq.kind = 0;
+            eq.D = ws.q4.f() + (size_t)fbase * np;
+            eq.ld = np;
+            eq.bias = h->pw.zero_np;
+            HIPC(launch_gemm(T + 1, np, h->feat, aq, bq, eq, st));
+            aq.R = ws.Rb.f();  // aux channels 0 .. A-2 (the I slice, as a4.r_off / n_aux)
+            bq.p = h->pw.M1T + (size_t)h->feat * np;
+            eq.D = ws.a4.f() + (size_t)fbase * np;
+            eq.bias = h->pw.bP1;
+            HIPC(launch_gemm(T + 1, np, h->A - 1, aq, bq, eq, st));
+            // the whole stream for the kernels that read it; step 0 only when every launch
+            // forms P1 in-kernel (k_persist_init reads step 0)
+            HIPC(launch_p1_expand(P1out, Btot, row0, Bu, h->p1_stream ? S : 1, tpo, L, h->hop, T,
+                                  np / 4, ws.q4.f() + (size_t)fbase * np,
+                                  ws.a4.f() + (size_t)fbase * np, h->pw.p1taps, st));
+        } else if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
             const int np = h->pw.p1x4 ? 4 * H : 3 * H;  // (fatchord: + cI, unit-major)
             b4.p = h->pw.M1T;
             b4.ld = np;
@@ -1607,6 +1753,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     a.oF2 = W.oF2;
     a.P1 = P.P1.f();
     a.cI = ws.cI.f();
+    if (h->p1_ring && !rr && !gen) {  // k_persist forms P1 in-kernel (wide launches ignore these)
+        a.p1q = ws.q4.f();
+        a.p1a = ws.a4.f();
+        a.p1taps = W.p1taps + (size_t)h->hop * 8;  // the [hop][4] table
+        a.p1split = W.p1split;
+    }
     a.gumbel = P.gumbel.f();
     a.labels = (int16_t*)ws.labels.p;
     a.samples = ws.samples.f();
@@ -1865,11 +2017,14 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         p.B = b;
         p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
         p.pbase = P;
-        p.fbase = Fr;
+        // frame slots: [guard][zero frame = fbase][T frames][guard][guard], consecutive
+        // utterances sharing one guard: the in-kernel P1 taps (frames f-2 .. f+2) then read
+        // zero rows past either end without bounds checks
+        p.fbase = Fr + 1;
         p.row0 = B;
         B += b;
         P += p.Lpad;
-        Fr += p.T + 1;
+        Fr += p.T + 3;
         Tmax = std::max(Tmax, p.T);
     }
     if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
@@ -1902,7 +2057,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
             const int w10 = h->pw.cpw > 16 ? 1 : 0;
             for (int c = 1; c <= kPNR; ++c) {
-                const int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode);
+                const int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, p1_ring_ok(h));
                 if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[w10][c]});
             }
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
@@ -1976,7 +2131,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     }
     const int Bp = use_p ? Bplan : B;  // persistent groups carry nr rows per launch
     h->p_plan = use_p ? lplan : std::vector<wrnn_handle::PLaunch>();
-    CHECK(ensure_workspace(h, Bp, S, P, Fr, Tmax));
+    // P1: the register-resident fatchord launches form it in-kernel (ring) when the per-frame
+    // form exists; the [S][B][4H] stream is written only for the other kernels
+    bool any_wide = false;
+    for (const auto& L : h->p_plan) any_wide |= L.wide;
+    h->p1_ring = use_p && p1_ring_ok(h);
+    h->p1_stream = use_p && (!h->p1_ring || any_wide);
+    CHECK(ensure_workspace(h, Bp, S, P, Fr + 1, Tmax));
     auto& ws = h->ws;
     h->last_B = B;
     h->last_Bp = Bp;
@@ -2004,7 +2165,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
                         hipMemcpyHostToDevice, h->stream));
     // upsample + conditioning per utterance (cI folded with row stride Bp)
-    if (use_p) CHECK(h->pws.P1.alloc((size_t)S * Bp * (h->pw.p1x4 ? 4 : 3) * kPH * sizeof(float)));
+    if (use_p)  // (ring only: step 0 for k_persist_init)
+        CHECK(h->pws.P1.alloc((size_t)(h->p1_stream ? S : 1) * Bp * (h->pw.p1x4 ? 4 : 3) * kPH * sizeof(float)));
     if (use_p) {  // noise on the side stream, concurrent with the upsample / conditioning GEMMs
         if (!h->side) {
             HIPC(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
@@ -2016,6 +2178,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         CHECK(persist_noise(h, S, h->side));
         HIPC(hipEventRecord(h->noise_done, h->side));
         h->noise_pending = true;
+    }
+    if (use_p && h->pw.p1x4 && h->pw.p1taps_ok && p1_frames_enabled()) {
+        // per-frame P1 projections of every utterance at its frame slots; guards stay zero
+        const size_t bytes = (size_t)ws.Fcap * 4 * h->H * sizeof(float);
+        CHECK(ws.q4.alloc(bytes));
+        CHECK(ws.a4.alloc(bytes));
+        HIPC(hipMemsetAsync(ws.q4.p, 0, bytes, h->stream));
     }
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
@@ -2452,11 +2621,53 @@ int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* a
     const size_t nm = (size_t)h->feat * h->last_L0, na = (size_t)h->R * h->last_T0;
     if (mel_out) {
         if (mel_cap < nm) return fail(WRNN_ERR_CAPACITY, "mel capacity");
+        if (!h->melup_valid)
+            return fail(WRNN_ERR_INVALID, "the last call did not materialise the upsampled mel "
+                                          "(persistent engine, per-frame P1): see wrnn_debug_p1");
         HIPC(hipMemcpy(mel_out, h->ws.melup.p, nm * sizeof(float), hipMemcpyDeviceToHost));
     }
     if (aux_out) {
         if (aux_cap < na) return fail(WRNN_ERR_CAPACITY, "aux capacity");
         HIPC(hipMemcpy(aux_out, h->ws.Rb.p, na * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return WRNN_OK;
+}
+
+int wrnn_debug_p1(wrnn_handle* h, int step, int row, float* out, size_t capacity) {
+    if (!h || !out) return fail(WRNN_ERR_INVALID, "null argument");
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->last_engine != WRNN_ENGINE_PERSIST || !h->pw.p1x4 || !h->pws.P1.p)
+        return fail(WRNN_ERR_INVALID, "the last call did not run the persistent engine");
+    const int np = 4 * h->H, Bp = h->last_Bp;
+    if (step < 0 || step >= h->last_S || row < 0 || row >= Bp)
+        return fail(WRNN_ERR_INVALID, "step / row out of range");
+    if (capacity < (size_t)np) return fail(WRNN_ERR_CAPACITY, "P1 capacity");
+    if (h->p1_stream || step == 0) {
+        HIPC(hipMemcpy(out, h->pws.P1.f() + ((size_t)step * Bp + row) * np, np * sizeof(float),
+                       hipMemcpyDeviceToHost));
+        return WRNN_OK;
+    }
+    // ring: the launch formed this step's P1 in-kernel; form it here from the same device
+    // tables with the same fp32 operations (k_persist p1_store / k_p1_expand)
+    const RowInfo ri = h->rows_host[row];
+    const int hop = h->hop, p = ri.rel0 + step, nfr = ri.L / hop;
+    const bool in = p < ri.L;
+    const int f = in ? p / hop : 0, s = in ? p - f * hop : 0;
+    std::vector<float> taps(8), q((size_t)np), a((size_t)np);
+    HIPC(hipMemcpy(taps.data(), h->pw.p1taps + (size_t)s * 8, 8 * sizeof(float), hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(a.data(), h->ws.a4.f() + (size_t)(in ? ri.fbase + 1 + f : ri.fbase) * np,
+                   np * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<float> m((size_t)np, 0.f);
+    for (int k = 0; k < 5; ++k) {
+        const int j = f - 2 + k;
+        const int slot = in && j >= 0 && j < nfr ? ri.fbase + 1 + j : ri.fbase;
+        HIPC(hipMemcpy(q.data(), h->ws.q4.f() + (size_t)slot * np, np * sizeof(float),
+                       hipMemcpyDeviceToHost));
+        for (int c = 0; c < np; ++c) m[c] = std::fma(taps[k], q[c], m[c]);
+    }
+    for (int c = 0; c < np; ++c) {
+        volatile float v = m[c] + a[c];
+        out[c] = v;
     }
     return WRNN_OK;
 }

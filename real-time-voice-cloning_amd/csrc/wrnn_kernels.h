@@ -141,6 +141,12 @@ hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, f
                               int scale, const float* w, int c, int out_lo, int out_len,
                               int ld_out, hipStream_t s);
 hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipStream_t s);
+// P1 [t][Btot][4 nq] of fold rows row0 .. row0 + Bu - 1 from the per-frame projections q / a
+// ([1 + T][4 nq], slot 0 = zero frame) and the upsampler's per-phase taps [hop][8] (runtime.hip
+// pack_p1): P1(p = hop f + s) = sum_k taps[s][k] q(f - 2 + k) + a(f), a(zero frame) for p >= L.
+hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int S, int tpo, int L, int hop,
+                            int T, int nq, const float* q, const float* a, const float* taps,
+                            hipStream_t s);
 
 // ---------------------------------------------------------------------------------------
 // Persistent, weight-stationary fatchord recurrence (kernels_persist.hip). 8 XCD-local groups
@@ -190,6 +196,14 @@ struct PersistArgs {
     int cond_width, oG2, oF1, oF2;
     const float* P1;        // [S][B][3H] = W_ih1 cI + b_ih1
     const float* cI;        // [S][B][H]
+    // P1 ring (k_persist, when p1q != nullptr): P1 (r, z, n, cI) of step t + 2 is formed in the
+    // launch by the unit's owner slot from the per-frame projections (runtime.hip pack_p1,
+    // the same arithmetic as k_p1_expand) and handed to every slot through the exchange area;
+    // then only k_persist_init reads P1 (step 0) and the [S][B][4H] stream is never written.
+    const float* p1q;       // [frame slots][4H]: M1_mel mel(frame), slot fbase = zero frame
+    const float* p1a;       // [frame slots][4H]: M1_aux aux(frame) + bP1 (zero frame: bP1)
+    const float* p1taps;    // [hop][4]: upsampler taps of frames f-2+k0 .. f+1+k0 at phase s,
+    int p1split;            // k0 = (s >= p1split)
     const float* gumbel;    // RAW [S][B][n] Gumbel noise; MOL [S][B][kMolNoise]
     int16_t* labels;        // [B][ld]
     float* samples;         // [B][ld]
@@ -315,8 +329,9 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
                             uint32_t k1, hipStream_t s);
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
                          uint32_t k0, uint32_t k1, hipStream_t s);
-int persist_variant_ok(int nr, int cpw, int mode);
-int persist_variant_scratch(int nr, int cpw, int mode);
+// ring: the P1-ring variant (PersistArgs::p1q set) or the P1-stream variant
+int persist_variant_ok(int nr, int cpw, int mode, int ring);
+int persist_variant_scratch(int nr, int cpw, int mode, int ring);
 size_t persist_lds_bytes();
 size_t persist_xbuf_floats();
 

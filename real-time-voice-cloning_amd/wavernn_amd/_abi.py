@@ -38,7 +38,7 @@ EXPORTED = [
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
-    'wrnn_debug_beta', 'wrnn_plan_info',
+    'wrnn_debug_beta', 'wrnn_plan_info', 'wrnn_debug_p1',
 ]
 
 
@@ -128,6 +128,7 @@ def load_library(path=None):
                                     P(ctypes.c_float)]),
         'wrnn_debug_upsample': (c_int, [c_void_p, P(ctypes.c_float), c_size_t,
                                         P(ctypes.c_float), c_size_t]),
+        'wrnn_debug_p1': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

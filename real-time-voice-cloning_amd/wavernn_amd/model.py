@@ -252,6 +252,15 @@ class WaveRNN:
                                                  aux.ctypes.data_as(fp), aux.size))
         return mel, aux
 
+    def debug_p1(self, step, row):
+        """PERSIST conditioning input of the last persistent call at (step, fold row):
+        (rnn_dims, 4) float32 per unit: r, z, n of W_ih1 (I c) + b_ih1, then I c + b_I."""
+        out = np.empty((self.rnn_dims, 4), dtype=np.float32)
+        _abi.check(self._lib.wrnn_debug_p1(self._h, step, row,
+                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                           out.size))
+        return out
+
     def gen_display(self, i, seq_len, b_size, gen_rate):
         pbar = _progbar(i, seq_len)
         msg = f'| {pbar} {i*b_size}/{seq_len*b_size} | Batch Size: {b_size} | Gen Rate: {gen_rate:.1f}kHz | '

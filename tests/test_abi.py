@@ -12,7 +12,7 @@ from conftest import REPO
 
 def declared_symbols():
     src = open(os.path.join(REPO, 'include', 'wavernn_mi355x.h')).read()
-    return sorted(set(re.findall(r'\b(wrnn_[a-z_]+)\s*\(', src)) - {'wrnn_progress_fn'})
+    return sorted(set(re.findall(r'\b(wrnn_[a-z0-9_]+)\s*\(', src)) - {'wrnn_progress_fn'})
 
 
 def test_header_and_binding_agree():

@@ -100,7 +100,9 @@ def test_upsample_network_matches_oracle():
     from oracle.wavernn_oracle import OracleWaveRNN
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    meta, gold, m, wav = run_case('fatchord_raw9_tiny')
+    # the CHAIN engine materialises the upsampled mel; PERSIST never does (per-frame P1,
+    # test_persist_p1_matches_oracle)
+    meta, gold, m, wav = run_case('fatchord_raw9_tiny', engine='chain')
     T = meta['n_frames']
     mel_up, aux = m.debug_upsample(T)
     hp = hparams_of(meta)
@@ -115,6 +117,54 @@ def test_upsample_network_matches_oracle():
     ref_mel = ref_mel[0].numpy().T
     np.testing.assert_allclose(aux, ref_aux, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(mel_up, ref_mel, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('case', ['fatchord_raw9_tiny', 'fatchord_raw10_unbatched_tiny',
+                                  'runtimeracer_raw10_defaults', 'geneing_bits9_defaults'])
+def test_persist_p1_matches_oracle(case):
+    """The persistent engines' conditioning input P1 (per-frame projections expanded by the
+    upsampler's per-phase taps, runtime.hip pack_p1 / kernels_gemm.hip k_p1_expand) equals
+    W_ih1 (I[:,1:] [mel_up(p), a1(p)] + b_I) + b_ih1 and I c + b_I computed in float64 from the
+    oracle's upsample network, at frame edges, mid-frame, step 0 / S-1 and the zero-padded tail
+    fold (fatchord_version.py:78-85,174-201, fold_with_overlap :290-340)."""
+    import torch
+    from oracle.wavernn_oracle import OracleWaveRNN
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold, m, wav = run_case(case, engine='persist')
+    hp = hparams_of(meta)
+    from wavernn_amd.synth import synth_state_dict
+    sd = synth_state_dict(hp, meta['model_type'], seed=meta['weight_seed'],
+                          logit_scale=meta['logit_scale'])
+    o = OracleWaveRNN(sd, hp, meta['model_type'])
+    T = meta['n_frames']
+    mel = torch.from_numpy(synth_mel(T, meta['mel_seed'])[None] / sp.max_abs_value)
+    with torch.no_grad():
+        padded = o.pad_tensor(mel.transpose(1, 2), pad=hp.pad, side='both').transpose(1, 2)
+        mel_up, aux = o.upsample(padded)  # (1, L, 80), (1, L, R)
+    mel_up = mel_up[0].double().numpy()
+    aux = aux[0].double().numpy()
+    L = mel_up.shape[0]
+    Iw = np.asarray(sd['I.weight'], dtype=np.float64)
+    Ib = np.asarray(sd['I.bias'], dtype=np.float64)
+    W1 = np.asarray(sd['rnn1.weight_ih_l0'], dtype=np.float64)
+    b1 = np.asarray(sd['rnn1.bias_ih_l0'], dtype=np.float64)
+    ad = Iw.shape[1] - 1 - mel_up.shape[1]
+    H = Iw.shape[0]
+    B, S = m.fold_shape(T, meta['batched'], meta['target'], meta['overlap'])
+    tpo = meta['target'] + meta['overlap'] if meta['batched'] else 0
+    steps = sorted({0, 1, 199, 200, 201, 399, 400, S // 2, S - 2, S - 1} & set(range(S)))
+    rows = sorted({0, B // 2, B - 1})
+    for r in rows:
+        for t in steps:
+            p = r * tpo + t
+            c = np.concatenate([mel_up[p], aux[p, :ad]]) if p < L else np.zeros(Iw.shape[1] - 1)
+            cI = Iw[:, 1:] @ c + Ib
+            ref = np.stack([*(W1 @ cI + b1).reshape(3, H), cI], axis=1)  # (H, 4)
+            got = m.debug_p1(t, r).astype(np.float64)
+            scale = max(1.0, np.abs(ref).max())
+            err = np.abs(got - ref).max()
+            assert err <= 2e-5 * scale, (case, r, t, p, err, scale)
 
 
 @pytest.mark.parametrize('case', ['fatchord_raw9_sharp_tiny', 'runtimeracer_raw9_tiny',
@@ -148,6 +198,32 @@ def test_persist_multi_row_groups_match_oracle(n_utts, case):
         got = lab[row_off[u]:row_off[u + 1]]
         assert np.array_equal(got, ref['labels']), \
             f'utt {u}: first divergence {first_divergence(got, ref["labels"])}'
+
+
+@pytest.mark.parametrize('case,n_utts', [('fatchord_raw9_sharp_tiny', 1), ('fatchord_raw9_sharp_tiny', 4),
+                                         ('fatchord_raw9_sharp_tiny', 10), ('fatchord_mol_tiny', 3),
+                                         ('fatchord_raw10_unbatched_tiny', 1)])
+def test_persist_p1_ring_equals_stream(case, n_utts, monkeypatch):
+    """k_persist forms P1 in-kernel (the owner slot of each unit, handed over through the
+    exchange area) with the same fp32 operations as k_p1_expand's [S][B][4H] stream: labels /
+    samples of the two forms are identical (WRNN_P1_RING=0 forces the stream), for 1-4 rows per
+    XCD group and consecutive row batches."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case(case)
+    m, hp, sd = make_model(meta)
+    mels = [synth_mel(meta['n_frames'], 200 + u) / sp.max_abs_value for u in range(n_utts)]
+    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
+    m.set_engine('persist')
+    out = []
+    for ring in ('1', '0'):
+        monkeypatch.setenv('WRNN_P1_RING', ring)
+        m.set_seed(meta['noise_seed'])
+        res, row_off, S = m.generate_batch_device(dev, meta['batched'], meta['target'], meta['overlap'])
+        assert m.last_engine() == 'persist'
+        out.append(res.cpu().numpy())
+    assert np.array_equal(out[0], out[1]), f'first divergence {first_divergence(out[0], out[1])}'
 
 
 @pytest.mark.parametrize('case', ['fatchord_mol_tiny', 'runtimeracer_mol_tiny', 'geneing_mol_tiny',
