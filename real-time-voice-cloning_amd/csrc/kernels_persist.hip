@@ -793,8 +793,17 @@ hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// RAW Gumbel noise g = -log(q), q the contract's Exp(1) variate (philox.h exp1_from_u32):
-// argmax_k (l_k + g_k) is the decision of argmax_k ((softmax(l)_k / sum) / q_k).
+// RAW Gumbel noise g = -log(q), q the contract's Exp(1) variate (philox.h exp1_from_u32, its
+// float64 log kept exact): argmax_k (l_k + g_k) is the decision of argmax_k ((softmax(l)_k / sum)
+// / q_k). The second log runs in fp32 (logf, ~1 ulp: the order of the fp32 rounding the
+// reference's own p / q carries) unless WRNN_GUMBEL_F64 is defined.
+__device__ __forceinline__ float gumbel_of(uint32_t x) {
+#ifdef WRNN_GUMBEL_F64
+    return (float)(-log((double)exp1_from_u32(x)));
+#else
+    return -logf(exp1_from_u32(x));
+#endif
+}
 __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int ng,
                                                 const RowInfo* rows, uint32_t k0, uint32_t k1) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r, k4)
@@ -806,10 +815,10 @@ __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int
     const RowInfo ri = rows[r];
     const U4 o = philox4x32_10((uint32_t)k4, (uint32_t)t, (uint32_t)ri.fold, ri.stream, k0, k1);
     float4 v;
-    v.x = (float)(-log((double)exp1_from_u32(o.x)));
-    v.y = (float)(-log((double)exp1_from_u32(o.y)));
-    v.z = (float)(-log((double)exp1_from_u32(o.z)));
-    v.w = (float)(-log((double)exp1_from_u32(o.w)));
+    v.x = gumbel_of(o.x);
+    v.y = gumbel_of(o.y);
+    v.z = gumbel_of(o.z);
+    v.w = gumbel_of(o.w);
     g[i] = v;
 }
 

@@ -67,9 +67,8 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
         rows, roff = None, [0]
     if world == 1:
         host = rows.cpu().numpy()
-        with ThreadPoolExecutor(threads) as ex:
-            return list(ex.map(lambda j: post_fn(host[roff[j]:roff[j + 1]], frames[mine[j]]),
-                               range(len(mine))))
+        return _map(lambda j: post_fn(host[roff[j]:roff[j + 1]], frames[mine[j]]),
+                    range(len(mine)), threads)
     # one gather of equal-shaped buffers (rows padded to the largest shard) to dst
     width = max(rows_of)
     dtype = rows.dtype if rows is not None else torch.int16
@@ -94,8 +93,20 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
             jobs.append((i, host[at:at + nf]))
             at += nf
     out = [None] * len(mels)
-    with ThreadPoolExecutor(threads) as ex:
-        for i, w in zip([j[0] for j in jobs],
-                        ex.map(lambda j: post_fn(j[1], frames[j[0]]), jobs)):
-            out[i] = w
+    for i, w in zip([j[0] for j in jobs], _map(lambda j: post_fn(j[1], frames[j[0]]), jobs, threads)):
+        out[i] = w
     return out
+
+
+_POOL = {}
+
+
+def _map(fn, items, threads):
+    """fn over items: inline for one item, else on a process-wide thread pool (created once:
+    a pool per call costs about a millisecond of thread start-up on the bench's path)."""
+    items = list(items)
+    if len(items) <= 1 or threads <= 1:
+        return [fn(x) for x in items]
+    if threads not in _POOL:
+        _POOL[threads] = ThreadPoolExecutor(threads)
+    return list(_POOL[threads].map(fn, items))
