@@ -13,10 +13,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-CORR = ("FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE reports half the bytes "
-        "of a wide coalesced read, 16 B/lane; this kernel's dominant stream, P1 and cI interleaved per "
-        "unit, is read with 16-B buffer loads; the 4-B/lane Gumbel-noise reads, about a fifth of the "
-        "stream, are a width the guide lists as uncalibrated); WRITE_SIZE as reported")
+CORR = ("FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE tallies the 128-B "
+        "memory requests of coalesced reads at 64 B); the dominant stream is the [S][B][4H] P1 "
+        "stream (16-B loads) for k_persist_wide / k_persist_rr / k_persist_gen and, for k_persist "
+        "(P1 formed in-kernel), the Gumbel noise (4-B lane loads, 256 B per wave) plus the per-frame "
+        "tables; WRITE_SIZE as reported")
 # workload -> (bench.py arguments as in tools/measure.sh ARGS, bench workload string, kernel key)
 def workload(model, wname, frames=1000, utts=1, target=11000, overlap=550):
     return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
