@@ -2057,7 +2057,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
             const int w10 = h->pw.cpw > 16 ? 1 : 0;
             for (int c = 1; c <= kPNR; ++c) {
-                const int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, p1_ring_ok(h));
+                int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 0);
+                if (p1_ring_ok(h)) {  // the call uses the flavour that spills less (below)
+                    const int sr = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 1);
+                    if (sr >= 0 && (sc < 0 || sr < sc)) sc = sr;
+                }
                 if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[w10][c]});
             }
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
@@ -2135,7 +2139,15 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // form exists; the [S][B][4H] stream is written only for the other kernels
     bool any_wide = false;
     for (const auto& L : h->p_plan) any_wide |= L.wide;
+    // per call: the ring unless a k_persist launch of the plan spills more with it than with
+    // the stream (measured: MOL at 3 rows per group spills one register with the ring and
+    // runs 6.87 against 6.53 us per step)
     h->p1_ring = use_p && p1_ring_ok(h);
+    for (const auto& L : h->p_plan)
+        if (h->p1_ring && !L.wide &&
+            persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
+                persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
+            h->p1_ring = false;
     h->p1_stream = use_p && (!h->p1_ring || any_wide);
     CHECK(ensure_workspace(h, Bp, S, P, Fr + 1, Tmax));
     auto& ws = h->ws;
