@@ -40,7 +40,8 @@ constexpr int XB_A_SZ = kPNR * 5 * kPH * 2;
 constexpr int XB_B = XB_A + 2 * XB_A_SZ;
 constexpr int XB_C = XB_B + kPNR * kPH * 2;
 constexpr int XB_D = XB_C + kPNR * kPH * 2;
-constexpr int XB_D_LOG = kPM * kPNR * 2;           // RAW candidates [slot][r][value, tag]
+// RAW candidates [slot][r][value, tag] or, per wave (WRNN_WAVE_CAND), [slot][r][wave 0-3][value, tag]
+constexpr int XB_D_LOG = kPM * kPNR * 4 * 2;
 constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
 constexpr int XB_G = XB_D + XB_D_SZ;              // gh1 [parity][r][unit] (r, z, n, -) float4
 constexpr int XB_G_SZ = 2 * kPNR * kPH * 4;
@@ -175,6 +176,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // issue theirs after the candidate publish, off the critical path (a wave polls only
     // with no bulk loads in flight: its first poll would wait for all of them).
     constexpr bool EARLY = !FC3R;  // sampling lanes: st = EARLY ? tid - 256 : tid in [0, 32 NR)
+#ifndef WRNN_WAVE_CAND
+#define WRNN_WAVE_CAND 0  // A/B: 6.75 vs 6.53 us per C2 step (slower), see DESIGN §3.0
+#endif
+    // RAW candidates per wave of 0-3 ([slot][r][wave]) instead of per slot through LDS
+    constexpr bool WCAND = WRNN_WAVE_CAND && !MOL && !FC3R;
     // Loads are unconditional (step indices clamped; past the last step the values go
     // unused): every path to the loop's back edge then consumes them, so the compiler's
     // wait insertion sees no load pending at the top of the step.
@@ -564,70 +570,112 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             } else {
                 fc3();
             }
-            float* red = lds + L_RED;  // [og][r][value, class]
-            if (kc < NR) {
-                float val = -INFINITY;
-                if (has_cls) {
-                    const float l = p_add(s0, lds[L_BCLS + og]);
-                    if (!MOL)
-                        val = p_add(l, pgum);
-                    else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
-                        bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
-                }
-                red[(og * kPNR + kc) * 2] = val;
-                red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
-            }
-            XSTAMP(28);
-            __syncthreads();
-            PSTAMP(11);
-            if (wv_lo) {
-            if (wave == 0) {
-                if (!MOL) {
-                    // slot candidate per row, tagged with the step (no flag, no wait)
-                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
-                    int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
-                    asm volatile("" : "+v"(tt));
-                    if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
-                        const int r = tt >> 4, o = tt & 15;
-                        float bv = -INFINITY;
-                        int bi = 0x7fffffff;
-                        if (r < NR && o < a.cpw) {
-                            bv = red[(o * kPNR + r) * 2];
-                            bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
-                        }
-                        row16_argmax(bv, bi);
-                        const int rr = r;
-                        if (r < NR && o == 0)
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
-                    } else {
+            // RAW, <= 16 classes per slot (WCAND): every wave of 0-3 publishes the candidate of
+            // its 4 classes per row straight from registers (shuffles over its 4 DPP rows), so
+            // no LDS round trip and no workgroup barrier sit between fc3 and the publish
+            if constexpr (WCAND) {
+                if (wv_lo) {
+                    float bv = -INFINITY;
+                    int bi = 0x7ff;
+                    if (kc < NR && has_cls) {
+                        const float l = p_add(s0, lds[L_BCLS + og]);
+                        bv = p_add(l, pgum);
+                        bi = cls;
+                    }
 #pragma unroll
-                        for (int rb = 0; rb < NR; rb += 2) {
-                            const int r = rb + (tt >> 5), o = tt & 31;
+                    for (int m = 16; m <= 32; m <<= 1) {  // lanes kc == r of the wave's 4 classes
+                        const float v2 = __shfl_xor(bv, m);
+                        const int k2 = __shfl_xor(bi, m);
+                        if (v2 > bv || (v2 == bv && k2 < bi)) {
+                            bv = v2;
+                            bi = k2;
+                        }
+                    }
+                    XSTAMP(28);
+                    if (kc < NR && (tid & 48) == 0) {
+                        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                        int kx = kc;  // (recomputed per step: hoisted offsets cost registers)
+                        asm volatile("" : "+v"(kx));
+                        __builtin_amdgcn_raw_buffer_store_b64(
+                            (u2v){__float_as_uint(bv), tag_hi | ((unsigned)bi & 0x7ffu)}, xr,
+                            (unsigned)(((w * kPNR + kx) * 4 + wave) * 2) * 4u, XB_D * 4, 0);
+                    }
+                    PSTAMP(11);
+                    if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
+                        gru1_loads();
+                        XSTAMP(27);
+                    }
+                } else if (NR > 2 && !WRNN_HH2_MAP) {
+                    PSTAMP(11);
+                    // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
+                    hh2_rows(std::integral_constant<int, 2>(), og - 16);
+                }
+            } else {
+                float* red = lds + L_RED;  // [og][r][value, class]
+                if (kc < NR) {
+                    float val = -INFINITY;
+                    if (has_cls) {
+                        const float l = p_add(s0, lds[L_BCLS + og]);
+                        if (!MOL)
+                            val = p_add(l, pgum);
+                        else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
+                            bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
+                    }
+                    red[(og * kPNR + kc) * 2] = val;
+                    red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
+                }
+                XSTAMP(28);
+                __syncthreads();
+                PSTAMP(11);
+                if (wv_lo) {
+                if (wave == 0) {
+                    if (!MOL) {
+                        // slot candidate per row, tagged with the step (no flag, no wait)
+                        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                        int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
+                        asm volatile("" : "+v"(tt));
+                        if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
+                            const int r = tt >> 4, o = tt & 15;
                             float bv = -INFINITY;
                             int bi = 0x7fffffff;
                             if (r < NR && o < a.cpw) {
                                 bv = red[(o * kPNR + r) * 2];
                                 bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                             }
-                            half_argmax(bv, bi);
+                            row16_argmax(bv, bi);
                             const int rr = r;
-                            if (r < NR && o == 31)
+                            if (r < NR && o == 0)
                                 __builtin_amdgcn_raw_buffer_store_b64(
                                     (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
                                     (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
+                        } else {
+    #pragma unroll
+                            for (int rb = 0; rb < NR; rb += 2) {
+                                const int r = rb + (tt >> 5), o = tt & 31;
+                                float bv = -INFINITY;
+                                int bi = 0x7fffffff;
+                                if (r < NR && o < a.cpw) {
+                                    bv = red[(o * kPNR + r) * 2];
+                                    bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                                }
+                                half_argmax(bv, bi);
+                                const int rr = r;
+                                if (r < NR && o == 31)
+                                    __builtin_amdgcn_raw_buffer_store_b64(
+                                        (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                        (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
+                            }
                         }
                     }
                 }
-            }
-            if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
-                gru1_loads();
-                XSTAMP(27);
-            }
-            } else {
-                // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
-                if (NR > 2 && !WRNN_HH2_MAP) hh2_rows(std::integral_constant<int, 2>(), og - 16);
+                if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
+                    gru1_loads();
+                    XSTAMP(27);
+                }
+                } else {
+                    // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
+                    if (NR > 2 && !WRNN_HH2_MAP) hh2_rows(std::integral_constant<int, 2>(), og - 16);
+                }
             }
         }
         if (FC3R) gru1_loads();
@@ -637,25 +685,56 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         if (!MOL) {
             if (st >= 0 && st < 32 * NR) {  // half-wave r: lane o polls slot o's candidate of row r
                 const int r = st >> 5, o = st & 31;
-                const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
                 const unsigned want = seq & kTagSeqMask;
                 const unsigned t0 = p_now();
                 unsigned n = 0;
-                u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
-                while (true) {  // two polls in flight (see poll_couples)
-                    const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
-                    if (__all((c.y >> 11) == want)) break;
-                    c = c1;
-                    if ((++n & 255) == 0) {
-                        if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
-                            if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
-                            lds[L_FAIL] = 1.f;
+                float bv;
+                int bi;
+                if constexpr (WCAND) {  // the slot's 4 wave candidates: two 16-byte loads
+                    const unsigned off = (unsigned)((o * kPNR + r) * 4 * 2) * 4u;
+                    u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off, XB_D * 4, kCpNT);
+                    u4v d = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, XB_D * 4, kCpNT);
+                    while (true) {  // two polls in flight (see poll_couples)
+                        const u4v c1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, XB_D * 4, kCpNT);
+                        const u4v d1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, XB_D * 4, kCpNT);
+                        if (__all((c.y >> 11) == want && (c.w >> 11) == want && (d.y >> 11) == want &&
+                                  (d.w >> 11) == want))
                             break;
+                        c = c1;
+                        d = d1;
+                        if ((++n & 255) == 0) {
+                            if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
+                                if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                                lds[L_FAIL] = 1.f;
+                                break;
+                            }
                         }
                     }
+                    // waves hold ascending classes: a later wave wins only when strictly larger
+                    bv = __uint_as_float(c.x);
+                    bi = (int)(c.y & 0x7ffu);
+                    const float v1 = __uint_as_float(c.z), v2 = __uint_as_float(d.x), v3 = __uint_as_float(d.z);
+                    if (v1 > bv) { bv = v1; bi = (int)(c.w & 0x7ffu); }
+                    if (v2 > bv) { bv = v2; bi = (int)(d.y & 0x7ffu); }
+                    if (v3 > bv) { bv = v3; bi = (int)(d.w & 0x7ffu); }
+                } else {
+                    const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
+                    u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
+                    while (true) {  // two polls in flight (see poll_couples)
+                        const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
+                        if (__all((c.y >> 11) == want)) break;
+                        c = c1;
+                        if ((++n & 255) == 0) {
+                            if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
+                                if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                                lds[L_FAIL] = 1.f;
+                                break;
+                            }
+                        }
+                    }
+                    bv = __uint_as_float(c.x);
+                    bi = (int)(c.y & 0x7ffu);
                 }
-                float bv = __uint_as_float(c.x);
-                int bi = (int)(c.y & 0x7ffu);
                 half_argmax(bv, bi);
                 if (o == 31) {
                     float xv;
