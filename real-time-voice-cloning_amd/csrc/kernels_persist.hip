@@ -353,15 +353,21 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         XSTAMP(30);
         PSTAMP(1);
         // ===== hop A: stage x2 -> X0, h2 -> XH2 (waves 0-3) ======================================
+#ifndef WRNN_H2_LATE
+#define WRNN_H2_LATE 1
+#endif
+        // H2_LATE: hop A waits for x2 only; waves 0-3 fetch h2 (published with x2, needed first
+        // by the off-path W_hh2 h2 of hop B) during stage B, where they are otherwise idle
+        constexpr int NA = WRNN_H2_LATE ? 1 : 2;  // arrays polled in hop A
         if (wv_lo) {  // polling the tagged pairs, one pass
-            unsigned off[2 * NR];
-            float2* dst[2 * NR];
+            unsigned off[NA * NR];
+            float2* dst[NA * NR];
 #pragma unroll
-            for (int m = 0; m < 2 * NR; ++m) {  // couple tl of (row m / 2, array m % 2)
-                off[m] = (unsigned)(((m >> 1) * 5 + (m & 1)) * kPH + 2 * tl) * 8u;
-                dst[m] = reinterpret_cast<float2*>(lds + ((m & 1) ? L_XH2 : L_X0) + (m >> 1) * kPH) + tl;
+            for (int m = 0; m < NA * NR; ++m) {  // couple tl of (row m / NA, array m % NA)
+                off[m] = (unsigned)(((m / NA) * 5 + (m % NA)) * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + ((m % NA) ? L_XH2 : L_X0) + (m / NA) * kPH) + tl;
             }
-            if (!poll_couples<2 * NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+            if (!poll_couples<NA * NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
@@ -400,6 +406,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             // gh1 (hop A) must be in L2 before this wave's y1 can be seen
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
+        } else if (WRNN_H2_LATE) {  // h2 -> XH2 (its tags were stored with x2's: one pass)
+            unsigned off[NR];
+            float2* dst[NR];
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                off[m] = (unsigned)((m * 5 + 1) * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + L_XH2 + m * kPH) + tl;
+            }
+            if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path, spread over the
         // exchange waits: rows r % 3 == 0 by waves 0-3 in hop B, r % 3 == 1 by waves 4-7 in hop
