@@ -119,20 +119,22 @@ __device__ __forceinline__ float mv1(const float4 (&wr)[kRNW], const float4* X, 
 // Poll one hop of NA arrays x NR rows x RH tagged pairs into LDS (dst0 / dst1 [kRNR][RH]);
 // every thread takes couples tid, tid + 512, ...; padding lanes re-poll a valid couple into a
 // sink. False on abort / timeout.
-template <int NR, int NA>
+// NT threads (tid < NT) poll arrays A0 .. A0 + NA - 1 of a buffer laid out with NL arrays per row
+// (GRU hops: NL = 2, x then h); dst0 / dst1 receive the first / second polled array.
+template <int NR, int NA, int NT = kPT, int NL = NA, int A0 = 0>
 __device__ __forceinline__ bool poll_hop(rsrc_t xr, unsigned so, unsigned seq, float* dst0,
                                          float* dst1, float* sink, unsigned* ctl, int tid) {
     constexpr int TOT = NR * NA * (RH / 2);
-    constexpr int M = (TOT + kPT - 1) / kPT;
+    constexpr int M = (TOT + NT - 1) / NT;
     unsigned off[M];
     float2* dst[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        const int c = tid + kPT * m;
+        const int c = tid + NT * m;
         const bool valid = c < TOT;
         const int cc = valid ? c : c % TOT;
         const int r = cc / (NA * (RH / 2)), a = (cc / (RH / 2)) % NA, cp = cc % (RH / 2);
-        off[m] = (unsigned)(((r * NA + a) * RH + 2 * cp) * 8);
+        off[m] = (unsigned)(((r * NL + A0 + a) * RH + 2 * cp) * 8);
         dst[m] = valid ? reinterpret_cast<float2*>((a ? dst1 : dst0) + r * RH) + cp
                        : reinterpret_cast<float2*>(sink);
     }
@@ -302,7 +304,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH4 + 16 + og]);
             }
         }
-        if (!poll_hop<NR, 2>(xr, sg(0), seq, lds + L_XB, lds + L_H2, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+#ifndef WRNN_RR_H_LATE
+#define WRNN_RR_H_LATE 1
+#endif
+        // H_LATE: each GRU hop waits for x only; idle quads fetch h2 / h3 / h4 in the next stage
+        // and the off-path W_hh2 h2 / W_hh3 h3 run one stage later (stages 3 / 4)
+        constexpr bool HL = WRNN_RR_H_LATE;
+        if (HL) {
+            if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(0), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else {
+            if (!poll_hop<NR, 2>(xr, sg(0), seq, lds + L_XB, lds + L_H2, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         // ================= stage 2: q0 GRU3 | q2 gh2 (next step) ============================
@@ -319,7 +331,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 bst_tag(hn, seq, xr, o_gh, sg(1));
             }
             __builtin_amdgcn_s_setprio(0);
-        } else if (q == 2) {
+        } else if (q == 2 && !HL) {
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             mv3<NR, 0>(wr, reinterpret_cast<const float4*>(lds + L_H2), kc, s0, s1, s2);
             if (own) {
@@ -328,8 +340,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 gh[RU * kRNR] = p_add(s1, cb[CB_HH2 + 8 + og]);
                 gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH2 + 16 + og]);
             }
+        } else if ((q & 1) && HL) {  // q1, q3: h2 of every slot (published with x2 at stage 1)
+            if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(0), seq, lds + L_H2, nullptr, sink, a.ctl,
+                                            ((q >> 1) << 7) | (tid & 127)))
+                lds[L_FAIL] = 1.f;
         }
-        if (!poll_hop<NR, 2>(xr, sg(1), seq, lds + L_XA, lds + L_H3, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        if (HL) {
+            if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(1), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else {
+            if (!poll_hop<NR, 2>(xr, sg(1), seq, lds + L_XA, lds + L_H3, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         // ================= stage 3: q1 GRU4 | q2 gh3 (next step) ============================
@@ -347,17 +367,29 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 bst_tag(hn, seq, xr, o_gh, sg(2));
             }
             __builtin_amdgcn_s_setprio(0);
-        } else if (q == 2) {
+        } else if (q == 2) {  // H_LATE: gh2 here (h2 staged in stage 2), gh3 in stage 4
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-            mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H3), kc, s0, s1, s2);
+            if (HL)
+                mv3<NR, 0>(wr, reinterpret_cast<const float4*>(lds + L_H2), kc, s0, s1, s2);
+            else
+                mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H3), kc, s0, s1, s2);
             if (own) {
-                float* gh = lds + L_GH3 + og * kRNR + kc;
-                gh[0] = p_add(s0, cb[CB_HH3 + og]);
-                gh[RU * kRNR] = p_add(s1, cb[CB_HH3 + 8 + og]);
-                gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH3 + 16 + og]);
+                const int ob = HL ? CB_HH2 : CB_HH3;
+                float* gh = lds + (HL ? L_GH2 : L_GH3) + og * kRNR + kc;
+                gh[0] = p_add(s0, cb[ob + og]);
+                gh[RU * kRNR] = p_add(s1, cb[ob + 8 + og]);
+                gh[2 * RU * kRNR] = p_add(s2, cb[ob + 16 + og]);
             }
+        } else if ((q == 0 || q == 3) && HL) {  // h3 of every slot (published with x3 at stage 2)
+            if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(1), seq, lds + L_H3, nullptr, sink, a.ctl,
+                                            ((q & 1) << 7) | (tid & 127)))
+                lds[L_FAIL] = 1.f;
         }
-        if (!poll_hop<NR, 2>(xr, sg(2), seq, lds + L_XB, lds + L_H4, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        if (HL) {
+            if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(2), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else {
+            if (!poll_hop<NR, 2>(xr, sg(2), seq, lds + L_XB, lds + L_H4, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         // GRU1 operands of the end of this step: every slot's gh1 is in L2 (drained before its
@@ -405,6 +437,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             const float s = mv1<NR, 12>(wr, XB, kc);
             if (own) bst_tag(p_add(s, pc0), seq, xr, o_f, sf(0));
             __builtin_amdgcn_s_setprio(0);
+        } else if (q == 2 && HL) {  // gh3 = W_hh3 h3 + b (next step's GRU3; h3 staged in stage 3)
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            mv3<NR, 12>(wr, reinterpret_cast<const float4*>(lds + L_H3), kc, s0, s1, s2);
+            if (own) {
+                float* gh = lds + L_GH3 + og * kRNR + kc;
+                gh[0] = p_add(s0, cb[CB_HH3 + og]);
+                gh[RU * kRNR] = p_add(s1, cb[CB_HH3 + 8 + og]);
+                gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH3 + 16 + og]);
+            }
         }
         if (!poll_hop<NR, 1>(xr, sf(0), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
@@ -418,6 +459,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 bst_tag(y > 0.f ? y : 0.f, seq, xr, o_f, sf(1));
             }
             __builtin_amdgcn_s_setprio(0);
+        } else if ((q & 1) && HL) {  // q1, q3: h4 of every slot (published with x4 at stage 3;
+                                     // their GRU1 loads have landed: the hop-4 poll waited on them)
+            if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(2), seq, lds + L_H4, nullptr, sink, a.ctl,
+                                            ((q >> 1) << 7) | (tid & 127)))
+                lds[L_FAIL] = 1.f;
         }
         if (!poll_hop<NR, 1>(xr, sf(1), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
