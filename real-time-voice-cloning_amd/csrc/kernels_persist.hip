@@ -57,6 +57,7 @@ constexpr int L_XH2 = L_X1 + kPNR * kPH;            // [kPNR][512] h2 (staged at
 constexpr int L_RED = L_XH2 + kPNR * kPH;           // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
+constexpr int L_SINK = L_SX + 14;                   // float2 sink of padding poll lanes
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
 constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
@@ -359,7 +360,29 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // H2_LATE: hop A waits for x2 only; waves 0-3 fetch h2 (published with x2, needed first
         // by the off-path W_hh2 h2 of hop B) during stage B, where they are otherwise idle
         constexpr int NA = WRNN_H2_LATE ? 1 : 2;  // arrays polled in hop A
-        if (wv_lo) {  // polling the tagged pairs, one pass
+#ifndef WRNN_HOPA_ALL
+#define WRNN_HOPA_ALL 0  // A/B: 6.38 vs 6.28 us per C2 step (slower)
+#endif
+        // HOPA_ALL: x2 polled by all 8 waves (waves 4-7 are done with W_hh1 by then): half the
+        // couples per lane
+        if (WRNN_H2_LATE && WRNN_HOPA_ALL) {
+            constexpr int TOT = NR * (kPH / 2), MA = (TOT + kPT - 1) / kPT;
+            unsigned off[MA];
+            float2* dst[MA];
+            int tx = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
+            asm volatile("" : "+v"(tx));
+#pragma unroll
+            for (int m = 0; m < MA; ++m) {
+                const int c = tx + kPT * m;
+                const bool valid = c < TOT;
+                const int cc = valid ? c : c - TOT;  // padding lanes re-poll a valid couple
+                const int r = cc / (kPH / 2), cp = cc % (kPH / 2);
+                off[m] = (unsigned)(r * 5 * kPH + 2 * cp) * 8u;
+                dst[m] = valid ? reinterpret_cast<float2*>(lds + L_X0 + r * kPH) + cp
+                               : reinterpret_cast<float2*>(lds + L_SINK);
+            }
+            if (!poll_couples<MA>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+        } else if (wv_lo) {  // polling the tagged pairs, one pass
             unsigned off[NA * NR];
             float2* dst[NA * NR];
 #pragma unroll
