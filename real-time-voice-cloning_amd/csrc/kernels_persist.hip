@@ -69,6 +69,13 @@ constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
+#ifndef WRNN_X2_LOCAL
+#define WRNN_X2_LOCAL 1  // hop A carries h2 only; every slot forms x2 = x1 + h2 (see hop A)
+#endif                   // (RAW only: MOL measured 6.28 vs 6.24 us per step with it)
+#ifndef WRNN_X2_LOCAL_MOL
+#define WRNN_X2_LOCAL_MOL 0
+#endif
+
 // P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
 template <int NR, bool FC3R, bool MOL, bool P1R>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // issue theirs after the candidate publish, off the critical path (a wave polls only
     // with no bulk loads in flight: its first poll would wait for all of them).
     constexpr bool EARLY = !FC3R;  // sampling lanes: st = EARLY ? tid - 256 : tid in [0, 32 NR)
+    constexpr bool X2L = MOL ? WRNN_X2_LOCAL_MOL : WRNN_X2_LOCAL;
 #ifndef WRNN_WAVE_CAND
 #define WRNN_WAVE_CAND 0  // A/B: 6.75 vs 6.53 us per C2 step (slower), see DESIGN §3.0
 #endif
@@ -339,7 +347,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2),
                                            gh2[0], gh2[kPNR], gh2[2 * kPNR], h2r);
                     h2r = hn;
-                    bst_tag(p_add(lds[L_X0 + lr * kPH + u], hn), seq, xr, o_u, sA);  // x2 = x1 + h2
+                    if (!X2L)  // (X2_LOCAL: every slot forms x2 = x1 + h2 itself)
+                        bst_tag(p_add(lds[L_X0 + lr * kPH + u], hn), seq, xr, o_u, sA);  // x2 = x1 + h2
                     bst_tag(hn, seq, xr, o_u, sA + kPH * 8);
                 } else {  // gh1 (r, z, n) of (row lr, unit u) for GRU1 at the end of this step
                     const float* b = lds + L_BIAS + (og - 16);  // b_hh1 of unit u
@@ -360,12 +369,36 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // H2_LATE: hop A waits for x2 only; waves 0-3 fetch h2 (published with x2, needed first
         // by the off-path W_hh2 h2 of hop B) during stage B, where they are otherwise idle
         constexpr int NA = WRNN_H2_LATE ? 1 : 2;  // arrays polled in hop A
+        // X2_LOCAL: x1 is the same in every slot (GRU1 runs redundantly), so hop A carries h2
+        // only and each poll lane forms x2 = x1 + h2 of its couples itself -- the producer's own
+        // fp32 add on the same operands (bit-identical x2), one publish instead of two, and no
+        // second poll for h2
 #ifndef WRNN_HOPA_ALL
 #define WRNN_HOPA_ALL 0  // A/B: 6.38 vs 6.28 us per C2 step (slower)
 #endif
         // HOPA_ALL: x2 polled by all 8 waves (waves 4-7 are done with W_hh1 by then): half the
         // couples per lane
-        if (WRNN_H2_LATE && WRNN_HOPA_ALL) {
+        if (X2L) {
+            if (wv_lo) {
+                unsigned off[NR];
+                float2* dst[NR];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {  // couple tl of row m: h2 -> XH2
+                    off[m] = (unsigned)((m * 5 + 1) * kPH + 2 * tl) * 8u;
+                    dst[m] = reinterpret_cast<float2*>(lds + L_XH2 + m * kPH) + tl;
+                }
+                if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {  // x2 = x1 + h2 of the same couples (own writes)
+                    float2* x = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
+                    const float2 h = *dst[m];
+                    float2 v = *x;
+                    v.x = p_add(v.x, h.x);
+                    v.y = p_add(v.y, h.y);
+                    *x = v;
+                }
+            }
+        } else if (WRNN_H2_LATE && WRNN_HOPA_ALL) {
             constexpr int TOT = NR * (kPH / 2), MA = (TOT + kPT - 1) / kPT;
             unsigned off[MA];
             float2* dst[MA];
@@ -429,7 +462,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             // gh1 (hop A) must be in L2 before this wave's y1 can be seen
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
-        } else if (WRNN_H2_LATE) {  // h2 -> XH2 (its tags were stored with x2's: one pass)
+        } else if (WRNN_H2_LATE && !X2L) {  // h2 -> XH2 (tags stored with x2's: one pass)
             unsigned off[NR];
             float2* dst[NR];
 #pragma unroll
