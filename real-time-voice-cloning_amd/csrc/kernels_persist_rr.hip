@@ -141,6 +141,41 @@ __device__ __forceinline__ bool poll_hop(rsrc_t xr, unsigned so, unsigned seq, f
     return poll_couples<M>(xr, off, so, seq, dst, ctl);
 }
 
+// GRU hop carrying h only (X_LOCAL): h -> hdst, and x_next = x_prev + h of the same couples
+// (the producer's own fp32 add on the same operands: x_prev is identical in every slot).
+template <int NR>
+__device__ __forceinline__ bool poll_hop_hx(rsrc_t xr, unsigned so, unsigned seq, float* hdst,
+                                            const float* xprev, float* xnext, float* sink,
+                                            unsigned* ctl, int tid) {
+    constexpr int TOT = NR * (RH / 2);
+    constexpr int M = (TOT + kPT - 1) / kPT;
+    unsigned off[M];
+    float2* dst[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int c = tid + kPT * m;
+        const bool valid = c < TOT;
+        const int cc = valid ? c : c % TOT;
+        const int r = cc / (RH / 2), cp = cc % (RH / 2);
+        off[m] = (unsigned)(((r * 2 + 1) * RH + 2 * cp) * 8);
+        dst[m] = valid ? reinterpret_cast<float2*>(hdst + r * RH) + cp : reinterpret_cast<float2*>(sink);
+    }
+    const bool ok = poll_couples<M>(xr, off, so, seq, dst, ctl);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int c = tid + kPT * m;
+        if (c < TOT) {
+            const int r = c / (RH / 2), cp = c % (RH / 2);
+            const float2 h = *dst[m];
+            float2 x = reinterpret_cast<const float2*>(xprev + r * RH)[cp];
+            x.x = p_add(x.x, h.x);
+            x.y = p_add(x.y, h.y);
+            reinterpret_cast<float2*>(xnext + r * RH)[cp] = x;
+        }
+    }
+    return ok;
+}
+
 }  // namespace
 
 template <int NR, bool MOL>
@@ -168,6 +203,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     const bool has_cls = cl < a.cpw && cls < a.n_classes;
     const int j = tid & (RH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
     constexpr int NRH = (NR + 1) / 2;
+#ifndef WRNN_RR_H_LATE
+#define WRNN_RR_H_LATE 1
+#endif
+    // H_LATE: each GRU hop waits for x only; idle quads fetch h2 / h3 / h4 in the next stage
+    // and the off-path W_hh2 h2 / W_hh3 h3 run one stage later (stages 3 / 4)
+    constexpr bool HL = WRNN_RR_H_LATE;
+#ifndef WRNN_RR_X_LOCAL
+#define WRNN_RR_X_LOCAL 1
+#endif
+    // X_LOCAL (with H_LATE): the GRU hops carry h only and every slot forms x itself
+    // (x1 is identical everywhere: GRU1 runs redundantly), so the late h polls go away
+    constexpr bool XL = HL && WRNN_RR_X_LOCAL;
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * RX_GROUP);
 
     // ---- weights -------------------------------------------------------------------------
@@ -277,7 +324,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                                        p_add(s2, cb[CB_IH2 + 16 + og]), gh[0], gh[RU * kRNR],
                                        gh[2 * RU * kRNR], h2r);
                 h2r = hn;
-                bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(0));
+                if (!XL) bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(0));
                 bst_tag(hn, seq, xr, o_gh, sg(0));
             }
             __builtin_amdgcn_s_setprio(0);
@@ -304,13 +351,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH4 + 16 + og]);
             }
         }
-#ifndef WRNN_RR_H_LATE
-#define WRNN_RR_H_LATE 1
-#endif
-        // H_LATE: each GRU hop waits for x only; idle quads fetch h2 / h3 / h4 in the next stage
-        // and the off-path W_hh2 h2 / W_hh3 h3 run one stage later (stages 3 / 4)
-        constexpr bool HL = WRNN_RR_H_LATE;
-        if (HL) {
+
+        if (XL) {
+            if (!poll_hop_hx<NR>(xr, sg(0), seq, lds + L_H2, lds + L_XA, lds + L_XB, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else if (HL) {
             if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(0), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         } else {
             if (!poll_hop<NR, 2>(xr, sg(0), seq, lds + L_XB, lds + L_H2, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
@@ -327,7 +371,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 const float hn = p_gru(p_add(s0, pc0), p_add(s1, pc1), p_add(s2, pc2), gh[0],
                                        gh[RU * kRNR], gh[2 * RU * kRNR], h3r);
                 h3r = hn;
-                bst_tag(p_add(lds[L_XB + kc * RH + u], hn), seq, xr, o_gx, sg(1));
+                if (!XL) bst_tag(p_add(lds[L_XB + kc * RH + u], hn), seq, xr, o_gx, sg(1));
                 bst_tag(hn, seq, xr, o_gh, sg(1));
             }
             __builtin_amdgcn_s_setprio(0);
@@ -340,12 +384,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 gh[RU * kRNR] = p_add(s1, cb[CB_HH2 + 8 + og]);
                 gh[2 * RU * kRNR] = p_add(s2, cb[CB_HH2 + 16 + og]);
             }
-        } else if ((q & 1) && HL) {  // q1, q3: h2 of every slot (published with x2 at stage 1)
+        } else if ((q & 1) && HL && !XL) {  // q1, q3: h2 of every slot (published with x2 at stage 1)
             if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(0), seq, lds + L_H2, nullptr, sink, a.ctl,
                                             ((q >> 1) << 7) | (tid & 127)))
                 lds[L_FAIL] = 1.f;
         }
-        if (HL) {
+        if (XL) {
+            if (!poll_hop_hx<NR>(xr, sg(1), seq, lds + L_H3, lds + L_XB, lds + L_XA, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else if (HL) {
             if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(1), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         } else {
             if (!poll_hop<NR, 2>(xr, sg(1), seq, lds + L_XA, lds + L_H3, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
@@ -363,7 +409,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                                        p_add(s2, cb[CB_IH4 + 16 + og]), gh[0], gh[RU * kRNR],
                                        gh[2 * RU * kRNR], h4r);
                 h4r = hn;
-                bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(2));
+                if (!XL) bst_tag(p_add(lds[L_XA + kc * RH + u], hn), seq, xr, o_gx, sg(2));
                 bst_tag(hn, seq, xr, o_gh, sg(2));
             }
             __builtin_amdgcn_s_setprio(0);
@@ -380,12 +426,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 gh[RU * kRNR] = p_add(s1, cb[ob + 8 + og]);
                 gh[2 * RU * kRNR] = p_add(s2, cb[ob + 16 + og]);
             }
-        } else if ((q == 0 || q == 3) && HL) {  // h3 of every slot (published with x3 at stage 2)
+        } else if ((q == 0 || q == 3) && HL && !XL) {  // h3 of every slot (published with x3 at stage 2)
             if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(1), seq, lds + L_H3, nullptr, sink, a.ctl,
                                             ((q & 1) << 7) | (tid & 127)))
                 lds[L_FAIL] = 1.f;
         }
-        if (HL) {
+        if (XL) {
+            if (!poll_hop_hx<NR>(xr, sg(2), seq, lds + L_H4, lds + L_XA, lds + L_XB, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
+        } else if (HL) {
             if (!poll_hop<NR, 1, kPT, 2, 0>(xr, sg(2), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         } else {
             if (!poll_hop<NR, 2>(xr, sg(2), seq, lds + L_XB, lds + L_H4, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
@@ -459,7 +507,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 bst_tag(y > 0.f ? y : 0.f, seq, xr, o_f, sf(1));
             }
             __builtin_amdgcn_s_setprio(0);
-        } else if ((q & 1) && HL) {  // q1, q3: h4 of every slot (published with x4 at stage 3;
+        } else if ((q & 1) && HL && !XL) {  // q1, q3: h4 of every slot (published with x4 at stage 3;
                                      // their GRU1 loads have landed: the hop-4 poll waited on them)
             if (!poll_hop<NR, 1, 256, 2, 1>(xr, sg(2), seq, lds + L_H4, nullptr, sink, a.ctl,
                                             ((q >> 1) << 7) | (tid & 127)))
