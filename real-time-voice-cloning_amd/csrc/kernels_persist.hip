@@ -30,6 +30,15 @@
 #include "persist_common.h"
 #include "philox.h"
 
+// The Makefile compiles this file twice, so that each half gets the machine-scheduler strategy
+// measured fastest for it on MI355X: part 1 = the categorical (RAW) variants,
+// the launch dispatch and the helper kernels, with the iterative ILP strategy; part 2 = the MOL
+// variants with the default strategy (ILP spills the MOL 3-row variant). Part 0 (the default)
+// is everything in one object (tools/build_variant.sh).
+#ifndef WRNN_PERSIST_PART
+#define WRNN_PERSIST_PART 0
+#endif
+
 namespace wrnn {
 
 // exchange area per group (floats). A, B, C hold tagged pairs (value bits, step + 1), so a
@@ -926,6 +935,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     }
 }
 
+#if WRNN_PERSIST_PART != 2
 // Step-0 state: GRU1 with x = 0, h = 0, gh = b_hh1 -> x1(0), h1(0); h2 = 0, gh2 = b_hh2.
 __global__ __launch_bounds__(kPT) void k_persist_init(PersistArgs a) {
     const int row = blockIdx.x, j = threadIdx.x, H = kPH;
@@ -1022,6 +1032,7 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
 
 size_t persist_lds_bytes() { return (size_t)L_TOTAL * sizeof(float); }
 size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
+#endif  // WRNN_PERSIST_PART != 2
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
@@ -1044,9 +1055,45 @@ int persist_spill_t() {
     return (int)fa.localSizeBytes;
 }
 
+#if WRNN_PERSIST_PART != 1
+// MOL variants (30 classes: cpw <= 16)
+int persist_spill_mol(int nr, int ring) {
+    switch (nr * 2 + (ring ? 1 : 0)) {
+        case 2: return persist_spill_t<1, false, true, false>();
+        case 3: return persist_spill_t<1, false, true, true>();
+        case 4: return persist_spill_t<2, false, true, false>();
+        case 5: return persist_spill_t<2, false, true, true>();
+        case 6: return persist_spill_t<3, false, true, false>();
+        case 7: return persist_spill_t<3, false, true, true>();
+        case 8: return persist_spill_t<4, false, true, false>();
+        case 9: return persist_spill_t<4, false, true, true>();
+        default: return -1;
+    }
+}
+
+hipError_t launch_persist_mol(const PersistArgs& a, hipStream_t s) {
+    const bool ring = a.p1q != nullptr;
+    switch (a.nr * 2 + (ring ? 1 : 0)) {
+        case 2: return launch_persist_t<1, false, true, false>(a, s);
+        case 3: return launch_persist_t<1, false, true, true>(a, s);
+        case 4: return launch_persist_t<2, false, true, false>(a, s);
+        case 5: return launch_persist_t<2, false, true, true>(a, s);
+        case 6: return launch_persist_t<3, false, true, false>(a, s);
+        case 7: return launch_persist_t<3, false, true, true>(a, s);
+        case 8: return launch_persist_t<4, false, true, false>(a, s);
+        case 9: return launch_persist_t<4, false, true, true>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+#else
+int persist_spill_mol(int nr, int ring);
+hipError_t launch_persist_mol(const PersistArgs& a, hipStream_t s);
+#endif
+
+#if WRNN_PERSIST_PART != 2
 template <int NR, bool P1R>
 int persist_spill_nr(int cpw, int mode) {
-    if (mode != 0) return cpw <= 16 ? persist_spill_t<NR, false, true, P1R>() : -1;  // MOL: 30 classes
+    if (mode != 0) return cpw <= 16 ? persist_spill_mol(NR, P1R) : -1;  // MOL: 30 classes
     return cpw > 16 ? persist_spill_t<NR, true, false, P1R>() : persist_spill_t<NR, false, false, P1R>();
 }
 
@@ -1075,7 +1122,7 @@ int persist_variant_ok(int nr, int cpw, int mode, int ring) {
 
 template <int NR, bool P1R>
 hipError_t launch_persist_nr(const PersistArgs& a, hipStream_t s) {
-    if (a.mode != 0) return a.cpw <= 16 ? launch_persist_t<NR, false, true, P1R>(a, s) : hipErrorInvalidValue;
+    if (a.mode != 0) return a.cpw <= 16 ? launch_persist_mol(a, s) : hipErrorInvalidValue;
     return a.cpw > 16 ? launch_persist_t<NR, true, false, P1R>(a, s) : launch_persist_t<NR, false, false, P1R>(a, s);
 }
 
@@ -1096,5 +1143,6 @@ hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 }
+#endif  // WRNN_PERSIST_PART != 2
 
 }  // namespace wrnn

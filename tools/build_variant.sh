@@ -13,6 +13,8 @@ for o in "$csrc"/build/*.o; do
   b=$(basename "$o" .o)
   skip=0
   for s in "$@"; do [ "$(basename "$s" .hip)" = "$b" ] && skip=1; done
+  # kernels_persist.hip rebuilt whole (part 0) replaces both of its default parts
+  [ "$b" = kernels_persist_mol ] && for s in "$@"; do [ "$s" = kernels_persist.hip ] && skip=1; done
   [ $skip = 0 ] && objs+=("$o")
 done
 for s in "$@"; do
