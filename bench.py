@@ -140,6 +140,32 @@ def _cpu_share():
     return n_aff, 'affinity mask'
 
 
+def _parity(r, gpu_rows, gpu_wav, seed, stream):
+    """GPU fold rows / waveform of one utterance against the oracle run `r` (same seed, stream)."""
+    import numpy as np
+    parity = {'rows': int(r['B']), 'steps': int(r['S']), 'seed': seed, 'stream': stream}
+    if r['labels'] is not None:
+        diff = np.argwhere(gpu_rows != r['labels'])
+        parity['labels_equal'] = bool(len(diff) == 0)
+        parity['label_agreement'] = float((gpu_rows == r['labels']).mean())
+        parity['first_divergence'] = (None if len(diff) == 0 else
+                                      [int(v) for v in diff[np.argmin(diff[:, 1])]])
+        parity['wave_bit_exact'] = bool(np.array_equal(gpu_wav, r['wav']))
+    else:
+        parity['samples_rms'] = float(np.sqrt(np.mean((gpu_rows.astype(np.float64) -
+                                                        r['samples']) ** 2)))
+        parity['wave_rms'] = float(np.sqrt(np.mean((gpu_wav - r['wav']) ** 2)))
+        parity['tolerance'] = 1e-4
+    return parity
+
+
+def parity_check(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
+    """The oracle on the host (default threads) for one utterance: parity only, not timed."""
+    import torch
+    r = _oracle_run(args, sd, hp, mel, torch.get_num_threads(), seed=seed, stream=stream)
+    return _parity(r, gpu_rows, gpu_wav, seed, stream)
+
+
 def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
     """The oracle (torch-CPU restatement of the reference generate(), pinned bit-exact to the
     reference by tests/test_oracle_golden.py) on this host's cores.
@@ -155,19 +181,7 @@ def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
     n_aff = len(os.sched_getaffinity(0))
     r = _oracle_run(args, sd, hp, mel, threads, seed=seed, stream=stream)
     samples = (args.frames - 1) * 200
-    parity = {'rows': int(r['B']), 'steps': int(r['S']), 'seed': seed, 'stream': stream}
-    if r['labels'] is not None:
-        diff = np.argwhere(gpu_rows != r['labels'])
-        parity['labels_equal'] = bool(len(diff) == 0)
-        parity['label_agreement'] = float((gpu_rows == r['labels']).mean())
-        parity['first_divergence'] = (None if len(diff) == 0 else
-                                      [int(v) for v in diff[np.argmin(diff[:, 1])]])
-        parity['wave_bit_exact'] = bool(np.array_equal(gpu_wav, r['wav']))
-    else:
-        parity['samples_rms'] = float(np.sqrt(np.mean((gpu_rows.astype(np.float64) -
-                                                        r['samples']) ** 2)))
-        parity['wave_rms'] = float(np.sqrt(np.mean((gpu_wav - r['wav']) ** 2)))
-        parity['tolerance'] = 1e-4
+    parity = _parity(r, gpu_rows, gpu_wav, seed, stream)
     legs = [dict(value=samples / r['t_wall'], unit='samples/s', cores=threads,
                  sample=f"whole utterance: {r['B']} folds x {r['S']} steps + upsample + post, "
                         f"{r['t_wall']:.1f}s")]
@@ -233,10 +247,13 @@ def main():
     if not args.no_timing:
         model.enable_stage_timing(True)
     last = {}
+    rows_dtype = torch.int16 if model.categorical else torch.float32
 
-    def rows_fn(ms):
-        out, roff, _ = model.generate_batch_device(ms, True, args.target, args.overlap)
-        last['rows'], last['roff'] = out, roff
+    def rows_fn(ms, streams):
+        # streams: the global utterance index offset by the step's base (distributed.py), so
+        # every utterance draws the same noise whatever the world size
+        out, roff, _ = model.generate_batch_device(ms, True, args.target, args.overlap,
+                                                   streams=streams)
         return out, roff
 
     def post_fn(rows, n_frames):
@@ -245,7 +262,13 @@ def main():
 
     def step():
         # the whole job: fold recurrence per rank, labels gathered to rank 0 (RCCL), f64 post
-        return infer_waveforms(mels, rows_fn, post_fn, args.target, args.overlap, S, device=dev)
+        base = model.get_stream()
+        rows = {}
+        w = infer_waveforms(mels, rows_fn, post_fn, args.target, args.overlap, S, device=dev,
+                            stream_base=base, dtype=rows_dtype, out_rows=rows)
+        model.set_stream(base + n_utts)  # every rank, whatever its shard
+        last['base'], last['rows'] = base, rows
+        return w
 
     for _ in range(args.warmup):
         wavs = step()
@@ -335,8 +358,8 @@ def main():
         result['config']['fallback_reason'] = fb[1]
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         # parity of the last timed call: utterance 0's fold rows and waveform against the oracle
-        gpu_rows = last['rows'].cpu().numpy()[last['roff'][0]:last['roff'][1]]
-        stream = (args.warmup + args.steps - 1) * U
+        gpu_rows = last['rows'][0]
+        stream = last['base']
         # PCIe-inclusive rate of the drop-in host-buffer API (WaveRNN.generate as
         # infer_waveform calls it: host mel in, f64 waveform out, the reference's progress
         # callback at i % 100 == 0 -- one persistent launch, progress read from host-mapped
@@ -354,6 +377,14 @@ def main():
                     'progress callback at i % 100 == 0 (reference cadence)'}
         result['cpu_baseline'], result['parity'] = cpu_baseline(args, sd, hp, mels_host[0],
                                                                 gpu_rows, wavs[0], seed, stream)
+    elif rank == 0 and world > 1 and args.cpu_seconds > 0:
+        # N > 1: one utterance of the LAST rank's shard, gathered over RCCL, against the oracle
+        # on its global stream (world-size invariance: the same labels as at N = 1)
+        u = plan[world - 1][0]
+        stream = last['base'] + u
+        result['parity'] = parity_check(args, sd, hp, mels_host[u], last['rows'][u], wavs[u],
+                                        seed, stream)
+        result['parity'].update(utterance=u, from_rank=world - 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

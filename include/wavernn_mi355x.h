@@ -129,6 +129,16 @@ int wrnn_load_bin(wrnn_handle* h, const void* data, size_t bytes);
 int wrnn_set_seed(wrnn_handle* h, uint64_t seed);
 /* Explicit stream id for the next call (advanced by one per utterance afterwards). */
 int wrnn_set_stream(wrnn_handle* h, uint32_t stream);
+/* Stream id the next call's first utterance will use. */
+int wrnn_get_stream(wrnn_handle* h, uint32_t* stream);
+/* Explicit noise stream of each utterance of the NEXT generate call only (n = its n_utts;
+ * n = 0 clears): utterance u draws from stream streams[u] instead of (stream + u), and the
+ * counter moves past the largest one afterwards. This is what makes sharded inference
+ * world-size invariant: every rank gives utterance i of the global batch the stream
+ * (base + i), as the reference's CPU backend seeds every worker instance explicitly
+ * (vocoder/libwavernn/inference.py:106-108, :200-204). A count that does not match the
+ * call's n_utts makes that call fail with WRNN_ERR_INVALID. */
+int wrnn_set_utt_streams(wrnn_handle* h, const uint32_t* streams, int n);
 
 /* Fold arithmetic of fold_with_overlap for a mel of n_frames frames
  * (upsampled length L = n_frames * hop). batched=0 -> one row of L steps. */
@@ -149,7 +159,8 @@ int wrnn_generate(wrnn_handle* h, const float* mel, int n_frames, int batched, i
  * pointers to (feat_dims, n_frames[u]) float32. Rows of all utterances run as one batch of
  * sum(num_folds) rows; row_offset[u] (host, n_utts+1 entries, filled by the call) gives each
  * utterance's first row. Outputs are DEVICE buffers of (total_rows, seq_len). Utterance u
- * uses noise stream (stream + u). Results are identical to n_utts single calls. */
+ * uses noise stream (stream + u), or streams[u] after wrnn_set_utt_streams. Results are
+ * identical to n_utts single calls with those streams. */
 int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* mels,
                                const int* n_frames, int batched, int target, int overlap,
                                int16_t* labels_dev, float* samples_dev, size_t capacity,
@@ -222,6 +233,16 @@ int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* a
  * per-frame form (taps of the upsampler over per-frame projections) the engines consume.
  * WRNN_ERR_INVALID when the last call did not run the persistent engine. */
 int wrnn_debug_p1(wrnn_handle* h, int step, int row, float* out, size_t capacity);
+
+/* Teacher-forced logit gate (SURVEY §7 "Hard parts" iii): later calls record the
+ * pre-sampling logits -- output of the last linear layer plus its bias, what the reference
+ * feeds to softmax / the MoL sampler (fatchord_version.py:213, runtimeracer_version.py:270) --
+ * of every fold row at up to 8 steps (n = 0 turns recording off). Recorded by the kernels that
+ * run the call (every persistent kernel and the CHAIN sampler); off, it costs one uniform
+ * branch per step. wrnn_debug_logits copies n_classes floats of (step, fold row) of the last
+ * call; WRNN_ERR_INVALID when that step was not recorded. */
+int wrnn_set_debug_steps(wrnn_handle* h, const int* steps, int n);
+int wrnn_debug_logits(wrnn_handle* h, int step, int row, float* out, size_t capacity);
 
 #ifdef __cplusplus
 }

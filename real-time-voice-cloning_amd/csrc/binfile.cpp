@@ -271,6 +271,11 @@ void stretch(Reader& r, int xs, int ys) {
 extern "C" int wrnn_bin_read(const void* data, size_t bytes, const wrnn_config* cfg, wrnn_tensor_fn fn,
                              void* user) {
     if (!data || !cfg || !fn) return bfail(WRNN_ERR_INVALID, "null argument");
+    // the topology comes from the caller: bound what indexes or shifts below
+    if (cfg->n_upsample < 1 || cfg->n_upsample > 4 || (cfg->mode == WRNN_MODE_RAW && (cfg->bits < 2 || cfg->bits > 12)) ||
+        cfg->res_blocks < 0 || cfg->res_blocks > 64 || cfg->rnn_dims <= 0 || cfg->fc_dims <= 0 ||
+        cfg->compute_dims <= 0 || cfg->res_out_dims <= 0 || cfg->feat_dims <= 0 || cfg->pad < 0)
+        return bfail(WRNN_ERR_INVALID, "libwavernn .bin: invalid model configuration");
     Reader r{static_cast<const uint8_t*>(data), bytes};
     Emitter E{fn, user};
     const int res_blocks = r.i32(), n_up = r.i32(), total_scale = r.i32(), pad = r.i32();

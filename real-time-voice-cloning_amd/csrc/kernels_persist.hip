@@ -696,6 +696,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     float val = -INFINITY;
                     if (has_cls) {
                         const float l = p_add(s0, lds[L_BCLS + og]);
+                        p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
                         if (!MOL)
                             val = p_add(l, pgum);
                         else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
@@ -906,7 +907,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             lds[L_X1 + r * kPH + tid] = hn;
         }
         pgum = pgn;
-        if (g == 0 && w == 0 && tid == 0) p_progress(a.progress, a.prog_base, t);
+        if (w == 0 && tid == 0) {
+            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen after hop A's barrier
+        }
         __syncthreads();
         PSTAMP(10);
     }
@@ -1044,6 +1048,8 @@ hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
+    static int coresident = 0;
+    if (hipError_t e = persist_coresident((const void*)k_persist<NR, FC3R, MOL, P1R>, lds, &coresident); e != hipSuccess) return e;
     hipLaunchKernelGGL((k_persist<NR, FC3R, MOL, P1R>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }

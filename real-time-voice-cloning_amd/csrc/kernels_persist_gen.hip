@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, bcls);
+                    p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
                     // (MOL / BETA: the logit itself, published after the gh1 poll below)
                     val = MODE == 0 ? p_add(l, pgum) : l;
                 }
@@ -431,7 +432,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                 lds[L_H1 + r * GH + j] = hn;
             }
         }
-        if (g == 0 && w == 0 && tid == 0) p_progress(a.progress, a.prog_base, t);
+        if (w == 0 && tid == 0) {
+            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next hop's check
+        }
         __syncthreads();
     }
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
@@ -483,6 +487,8 @@ hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
+    static int coresident = 0;
+    if (hipError_t e = persist_coresident((const void*)k_persist_gen<NR, MODE>, lds, &coresident); e != hipSuccess) return e;
     hipLaunchKernelGGL((k_persist_gen<NR, MODE>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }

@@ -437,9 +437,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     float s = 0.f;
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + cul];
-                    val = p_add(p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + 96 + cul]
-                                                            : bld(mk_rsrc(a.b_fc3), (unsigned)cu * 4u, 0)),
-                                pg);
+                    const float lg = p_add(s, lds[WL_BIAS + 96 + cul]);
+                    p_dbg_logit(a.dbg, t, crow, cu, a.B, a.n_classes, lg);
+                    val = p_add(lg, pg);
                 }
                 row16_argmax(val, cls);
                 if (cell && cul == 0)
@@ -506,7 +506,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
         }
-        if (g == 0 && w == 0 && tid == 0) p_progress(a.progress, a.prog_base, t);
+        if (w == 0 && tid == 0) {
+            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            if (p_abort(a.ctl, a.progress, t)) lds[WL_FAIL] = 1.f;  // seen after the next barrier
+        }
         WSTAMP(11);
     }
 #undef WSTAMP
@@ -538,6 +541,8 @@ hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
     }
+    static int coresident = 0;
+    if (hipError_t e = persist_coresident((const void*)k_persist_wide, lds, &coresident); e != hipSuccess) return e;
     hipLaunchKernelGGL(k_persist_wide, dim3(kPG * kPM), dim3(kPT), lds, s, a);
     return hipGetLastError();
 }

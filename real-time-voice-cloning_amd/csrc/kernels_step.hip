@@ -435,6 +435,13 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
             }
         }
     }
+    // teacher-forced logit gate (debug only): this row's logits at a recorded step
+    if (a.t >= 0 && a.dbg.out != nullptr) {
+        const int k = a.dbg.map[a.t];
+        if (k >= 0)
+            for (int c = tid; c < n; c += kThreads)
+                a.dbg.out[((size_t)k * a.nrows + r) * n + c] = a.logits[(size_t)r * n + c];
+    }
     float x = 0.f;
     if (a.t >= 0) {
         if (a.mode == 0) {

@@ -2,6 +2,9 @@
 // kernels_persist_rr.hip: runtimeracer): timers, DPP reductions, gate nonlinearities, buffer
 // resource access, tagged-pair exchanges over the XCD-shared L2.
 #pragma once
+#include <cstdlib>
+#include <cstring>
+
 #include "wrnn_kernels.h"
 
 namespace wrnn {
@@ -100,6 +103,26 @@ __device__ __forceinline__ int p_register(unsigned* ctl, int& group, int& slot) 
     return 1;
 }
 
+// Host side, before every persistent launch: can the launch's kPG * kPM workgroups be
+// co-resident on this device (occupancy query at the launch's dynamic LDS, x the CU count)?
+// A launch that could not be fails here in microseconds (hipErrorCooperativeLaunchTooLarge,
+// reported by the runtime as "cannot become co-resident") instead of spinning in p_register.
+// The answer is cached per kernel variant (`cached`: 0 unknown, 1 yes, 2 no). Test hook:
+// WRNN_DEBUG_PERSIST_FAIL=occupancy makes the check fail.
+inline hipError_t persist_coresident(const void* fn, size_t lds, int* cached) {
+    if (const char* e = std::getenv("WRNN_DEBUG_PERSIST_FAIL"))
+        if (!std::strcmp(e, "occupancy")) return hipErrorCooperativeLaunchTooLarge;
+    if (*cached == 0) {
+        int dev = 0, cus = 0, nb = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kPT, lds);
+        if (e != hipSuccess) return e;
+        *cached = nb * cus >= kPG * kPM ? 1 : 2;
+    }
+    return *cached == 1 ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
+}
+
 // Progress of a launch for the host's progress callback (fatchord_version.py:234-236 calls
 // back at i % 100 == 0): after step t with t % 100 == 0, one lane publishes base + t + 1
 // steps done to a host-mapped word (vector store, system scope); the host polls it while the
@@ -107,6 +130,28 @@ __device__ __forceinline__ int p_register(unsigned* ctl, int& group, int& slot) 
 __device__ __forceinline__ void p_progress(unsigned* prog, int base, int t) {
     if (prog != nullptr && t % kProgressEvery == 0)
         __hip_atomic_store(prog, (unsigned)(base + t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Abort request of the host (the progress callback returned non-zero): the host sets the
+// host-mapped word kAbortWord words past the progress word. At its progress points (every 100
+// steps, and only when a callback is registered) slot 0 of EVERY group reads it; on a request
+// it sets PC_ERR = 4 and returns true, and its workgroup exits at its next failure check --
+// the group's other workgroups then give up at their next spin check, so the launch (and,
+// through PC_ERR at registration, every queued launch of the call) drains within ~100 steps.
+__device__ __forceinline__ bool p_abort(unsigned* ctl, const unsigned* prog, int t) {
+    if (prog == nullptr || t % kProgressEvery != 0) return false;
+    if (__hip_atomic_load(prog + kAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) return false;
+    atomicMax(ctl + PC_ERR, 4u);
+    return true;
+}
+
+// Teacher-forced logit gate (debug only): the logit l of (row, cls) at a step the host asked
+// for goes to dbg.out[slot][row][cls] (wrnn_debug_logits); nothing when the capture is off.
+__device__ __forceinline__ void p_dbg_logit(const DbgLogits& d, int t, int row, int cls, int B,
+                                            int n, float l) {
+    if (d.out == nullptr) return;
+    const int k = __builtin_amdgcn_readfirstlane(d.map[t]);
+    if (k >= 0) d.out[((size_t)k * B + row) * n + cls] = l;
 }
 
 __device__ __forceinline__ int p_frame(const RowInfo& ri, int t, int hop) {

@@ -131,6 +131,14 @@ struct wrnn_handle {
     bool finalized = false;
     uint64_t seed = 0;
     uint32_t stream_ctr = 0;
+    std::vector<uint32_t> utt_streams;  // wrnn_set_utt_streams: explicit streams of the next call
+    // teacher-forced logit gate (wrnn_set_debug_steps): the steps to record, the device map
+    // [S] step -> slot and the capture [kDbgSteps][Bp][n] of the last call; dbg_gen keys the
+    // captured CHAIN graphs (their k_sample arguments hold the buffers)
+    std::vector<int> dbg_steps;
+    DevBuf dbg_out, dbg_map;
+    int dbg_gen = 0, dbg_rows = 0, dbg_S = 0;
+    DbgLogits dbg{};
 
     // ---- device weights
     std::vector<std::shared_ptr<DevBuf>> wbufs;
@@ -1409,6 +1417,7 @@ int launch_step(wrnn_handle* h, int t, int S, bool timing) {
     sa.k0 = (uint32_t)(h->seed & 0xffffffffu);
     sa.k1 = (uint32_t)(h->seed >> 32);
     sa.phases = nullptr;
+    sa.dbg = h->dbg;
     if (t == h->phase_step && h->phases.p)
         sa.phases = (uint32_t*)h->phases.p + h->stages.size() * kMaxStampWG * 8;
     HIPC(launch_sample(sa, st));
@@ -1459,7 +1468,7 @@ int run_chunk(wrnn_handle* h, int t0, int len, int S) {
     const bool last = t0 + len >= S;
     const int key_S = last ? S : -1;
     auto key = std::make_tuple(t0, len, key_S, h->last_B,
-                               (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1),
+                               (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1) | (h->dbg_gen << 24),
                                h->cfg.mode != WRNN_MODE_RAW ? h->seed : (uint64_t)0);
     auto it = h->graphs.find(key);
     if (it == h->graphs.end()) {
@@ -1760,6 +1769,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.p1split = W.p1split;
     }
     a.gumbel = P.gumbel.f();
+    a.dbg = h->dbg;
     a.labels = (int16_t*)ws.labels.p;
     a.samples = ws.samples.f();
     a.ld = ws.S;
@@ -1805,6 +1815,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         ag.st = P.st.f();
         ag.k0 = (uint32_t)(h->seed & 0xffffffffu);
         ag.k1 = (uint32_t)(h->seed >> 32);
+        ag.dbg = h->dbg;
         HIPC(launch_persist_gen_init(ag, st));
     } else if (rr) {
         ar.ctl = a.ctl;
@@ -1841,12 +1852,13 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         ar.samples = a.samples;
         ar.ld = a.ld;
         ar.st = P.st.f();
+        ar.dbg = h->dbg;
         HIPC(launch_persist_rr_init(ar, st));
     } else {
         HIPC(launch_persist_init(a, st));
     }
     HIPC(hipMemsetAsync(P.ctl.p, 0, PC_WORDS * sizeof(unsigned), st));
-    if (std::getenv("WRNN_DEBUG_PERSIST_FAIL")) {
+    if (const char* inj = std::getenv("WRNN_DEBUG_PERSIST_FAIL"); inj && std::strcmp(inj, "occupancy")) {
         // test hook: the call's launches find a co-residency error already set at registration
         // and exit, exercising the real failure path (fallback / error, warning, counters)
         static const unsigned kInjected = 1u;
@@ -1859,11 +1871,14 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int nb = (int)h->p_plan.size();
     a.wwide = (const float4*)W.wwide;
     a.wwide_lds = (const float4*)W.wwide_lds;
-    if (cb && !h->prog_host) {
-        HIPC(hipHostMalloc((void**)&h->prog_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    if (cb && !h->prog_host) {  // progress word + abort word (kAbortWord), two cache lines
+        HIPC(hipHostMalloc((void**)&h->prog_host, 128, hipHostMallocMapped | hipHostMallocCoherent));
         HIPC(hipHostGetDevicePointer((void**)&h->prog_dev, h->prog_host, 0));
     }
-    if (cb) __atomic_store_n(h->prog_host, 0u, __ATOMIC_RELAXED);
+    if (cb) {
+        __atomic_store_n(h->prog_host, 0u, __ATOMIC_RELAXED);
+        __atomic_store_n(h->prog_host + kAbortWord, 0u, __ATOMIC_RELAXED);
+    }
     a.progress = ag.progress = ar.progress = cb ? h->prog_dev : nullptr;
     for (auto e : h->pev) (void)hipEventDestroy(e);
     h->pev.clear();
@@ -1895,6 +1910,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             h->pev_rows.push_back(kPG * L.nr);
             HIPC(hipEventRecord(e0, st));
         }
+        hipError_t le;
         if (gen) {
             ag.t0 = a.t0;
             ag.t1 = a.t1;
@@ -1902,7 +1918,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ag.rb = a.rb;
             ag.stamps = a.stamps;
             ag.prog_base = a.prog_base;
-            HIPC(launch_persist_gen(ag, st));
+            le = launch_persist_gen(ag, st);
         } else if (rr) {
             ar.t0 = a.t0;
             ar.t1 = a.t1;
@@ -1910,16 +1926,31 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.rb = a.rb;
             ar.stamps = a.stamps;
             ar.prog_base = a.prog_base;
-            HIPC(launch_persist_rr(ar, st));
+            le = launch_persist_rr(ar, st);
         } else if (L.wide) {
-            HIPC(launch_persist_wide(a, st));
+            le = launch_persist_wide(a, st);
         } else {
-            HIPC(launch_persist(a, st));
+            le = launch_persist(a, st);
         }
+        if (le == hipErrorCooperativeLaunchTooLarge) {
+            // occupancy check of the launch wrapper: the grid cannot be co-resident, so the
+            // launch was not made (no spinning); the call falls back / fails at once
+            (void)hipStreamSynchronize(st);
+            fail(WRNN_ERR_HIP, "persistent launch: workgroups cannot become co-resident (occupancy "
+                               "check: fewer than 256 workgroups of 512 threads fit the device at once)");
+            return kPersistFallback;
+        }
+        if (le != hipSuccess)
+            return fail(WRNN_ERR_HIP, std::string("persistent launch: ") + hipGetErrorString(le));
         if (h->timing) HIPC(hipEventRecord(e1, st));
     }
+    // the launches' error word is read only once they have finished (a copy into pageable
+    // host memory queued here would block this thread until then, and every callback would
+    // come after the fact)
     unsigned err = 0;
-    HIPC(hipMemcpyAsync(&err, (unsigned*)P.ctl.p + PC_ERR, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    auto read_err = [&]() -> hipError_t {
+        return hipMemcpy(&err, (unsigned*)P.ctl.p + PC_ERR, sizeof(unsigned), hipMemcpyDeviceToHost);
+    };
     int rc = WRNN_OK;
     if (cb) {
         // report i = 0, 100, 200, ... < S in order, each once, when every row has finished step i
@@ -1938,14 +1969,24 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
                 break;
             }
             const bool finished = q == hipSuccess;
-            if (finished && err) break;  // failed launch: no progress to report
+            if (finished) {
+                if (read_err() != hipSuccess) {
+                    rc = fail(WRNN_ERR_HIP, "persistent launch: reading its error word");
+                    break;
+                }
+                if (err) break;  // failed launch: no progress to report
+            }
             const long long done = finished ? (long long)nb * S
                                             : (long long)__atomic_load_n(h->prog_host, __ATOMIC_RELAXED);
             const long long i_done = done / nb;  // steps every row has completed
             while (rc == WRNN_OK && next < S && next + 1 <= i_done) {
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-                if (cb(user, (int)next, S, B, (double)(next + 1) / std::max(el, 1e-9) * B / 1000.0))
+                if (cb(user, (int)next, S, B, (double)(next + 1) / std::max(el, 1e-9) * B / 1000.0)) {
+                    // the reference stops at the raising step: ask the launches to drain
+                    // (every group checks the word at its next progress point)
+                    __atomic_store_n(h->prog_host + kAbortWord, 1u, __ATOMIC_RELAXED);
                     rc = fail(WRNN_ERR_ABORTED, "aborted by progress callback");
+                }
                 next += kProgressEvery;
             }
             if (!finished && next < S) std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -1954,10 +1995,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     }
     HIPC(hipStreamSynchronize(st));
     if (rc) return rc;
+    HIPC(read_err());
     if (err) {
         static const char* what[] = {"", "workgroups did not become co-resident",
-                                     "exchange timeout", "workgroups not spread 32 per XCD"};
-        fail(WRNN_ERR_HIP, std::string("persistent launch: ") + (err < 4 ? what[err] : "unknown error"));
+                                     "exchange timeout", "workgroups not spread 32 per XCD",
+                                     "aborted"};
+        fail(WRNN_ERR_HIP, std::string("persistent launch: ") + (err < 5 ? what[err] : "unknown error"));
         return kPersistFallback;
     }
     if (a.phase_t >= 0) persist_phase_report(h, a.phase_t);
@@ -1988,6 +2031,34 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         it->rows += real;
         it->launches += 1;
     }
+    return WRNN_OK;
+}
+
+// Logit capture of this call (wrnn_set_debug_steps): map[t] = slot of step t (or -1), the
+// capture buffer NaN-filled so an unwritten entry shows. Off: null pointers in every launch.
+int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
+    const bool on = !h->dbg_steps.empty();
+    const void* out0 = h->dbg_out.p;
+    const void* map0 = h->dbg_map.p;
+    if (!on) {
+        if (h->dbg.out) ++h->dbg_gen;
+        h->dbg = DbgLogits{};
+        h->dbg_rows = 0;
+        return WRNN_OK;
+    }
+    const size_t n_out = (size_t)kDbgSteps * Bp * h->n_classes;
+    CHECK(h->dbg_out.alloc(n_out * sizeof(float)));
+    CHECK(h->dbg_map.alloc((size_t)S * sizeof(int)));
+    std::vector<int> map((size_t)S, -1);
+    for (size_t k = 0; k < h->dbg_steps.size(); ++k)
+        if (h->dbg_steps[k] < S) map[h->dbg_steps[k]] = (int)k;
+    HIPC(hipMemcpyAsync(h->dbg_map.p, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+    HIPC(hipMemsetAsync(h->dbg_out.p, 0xff, n_out * sizeof(float), h->stream));  // NaN
+    if (!h->dbg.out || out0 != h->dbg_out.p || map0 != h->dbg_map.p) ++h->dbg_gen;
+    h->dbg.out = h->dbg_out.f();
+    h->dbg.map = (const int*)h->dbg_map.p;
+    h->dbg_rows = Bp;
+    h->dbg_S = S;
     return WRNN_OK;
 }
 
@@ -2028,6 +2099,12 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         Tmax = std::max(Tmax, p.T);
     }
     if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
+    // explicit per-utterance noise streams (wrnn_set_utt_streams) are consumed by this call
+    std::vector<uint32_t> ustreams;
+    ustreams.swap(h->utt_streams);
+    if (!ustreams.empty() && (int)ustreams.size() != n_utts)
+        return fail(WRNN_ERR_INVALID, "wrnn_set_utt_streams gave " + std::to_string(ustreams.size()) +
+                                          " streams for a call of " + std::to_string(n_utts) + " utterances");
     // engine: PERSIST when asked for / automatic and the call qualifies
     int want = h->engine;
     if (const char* env = std::getenv("WRNN_ENGINE")) {
@@ -2167,7 +2244,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             ri.L = p.L;
             ri.fbase = p.fbase;
             ri.fold = f;
-            ri.stream = h->stream_ctr + (uint32_t)u;
+            ri.stream = ustreams.empty() ? h->stream_ctr + (uint32_t)u : ustreams[u];
         }
         if (row_offset) row_offset[u] = p.row0;
     }
@@ -2176,6 +2253,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     h->rows_host = rows;
     HIPC(hipMemcpyAsync(ws.rows.p, rows.data(), rows.size() * sizeof(RowInfo),
                         hipMemcpyHostToDevice, h->stream));
+    CHECK(setup_debug_logits(h, S, Bp));
     // upsample + conditioning per utterance (cI folded with row stride Bp)
     if (use_p)  // (ring only: step 0 for k_persist_init)
         CHECK(h->pws.P1.alloc((size_t)(h->p1_stream ? S : 1) * Bp * (h->pw.p1x4 ? 4 : 3) * kPH * sizeof(float)));
@@ -2238,7 +2316,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     h->last_engine = use_p ? WRNN_ENGINE_PERSIST : WRNN_ENGINE_CHAIN;
     if (use_p) h->persist_fail_streak = 0;
     if (seq_len) *seq_len = S;
-    h->stream_ctr += (uint32_t)n_utts;
+    if (ustreams.empty()) h->stream_ctr += (uint32_t)n_utts;
+    else h->stream_ctr = *std::max_element(ustreams.begin(), ustreams.end()) + 1u;
     return WRNN_OK;
 }
 
@@ -2421,6 +2500,19 @@ int wrnn_set_seed(wrnn_handle* h, uint64_t seed) {
 int wrnn_set_stream(wrnn_handle* h, uint32_t stream) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
     h->stream_ctr = stream;
+    return WRNN_OK;
+}
+
+int wrnn_get_stream(wrnn_handle* h, uint32_t* stream) {
+    if (!h || !stream) return fail(WRNN_ERR_INVALID, "null argument");
+    *stream = h->stream_ctr;
+    return WRNN_OK;
+}
+
+int wrnn_set_utt_streams(wrnn_handle* h, const uint32_t* streams, int n) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (n < 0 || (n > 0 && !streams)) return fail(WRNN_ERR_INVALID, "bad stream list");
+    h->utt_streams.assign(streams, streams + n);
     return WRNN_OK;
 }
 
@@ -2642,6 +2734,32 @@ int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* a
         if (aux_cap < na) return fail(WRNN_ERR_CAPACITY, "aux capacity");
         HIPC(hipMemcpy(aux_out, h->ws.Rb.p, na * sizeof(float), hipMemcpyDeviceToHost));
     }
+    return WRNN_OK;
+}
+
+int wrnn_set_debug_steps(wrnn_handle* h, const int* steps, int n) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (n < 0 || n > kDbgSteps || (n > 0 && !steps))
+        return fail(WRNN_ERR_INVALID, "at most " + std::to_string(kDbgSteps) + " debug steps");
+    for (int i = 0; i < n; ++i)
+        if (steps[i] < 0) return fail(WRNN_ERR_INVALID, "negative debug step");
+    h->dbg_steps.assign(steps, steps + n);
+    return WRNN_OK;
+}
+
+int wrnn_debug_logits(wrnn_handle* h, int step, int row, float* out, size_t capacity) {
+    if (!h || !out) return fail(WRNN_ERR_INVALID, "null argument");
+    HIPC(hipStreamSynchronize(h->stream));
+    if (!h->dbg.out) return fail(WRNN_ERR_INVALID, "the last call recorded no logits (wrnn_set_debug_steps)");
+    int k = -1;
+    for (size_t i = 0; i < h->dbg_steps.size(); ++i)
+        if (h->dbg_steps[i] == step) k = (int)i;
+    if (k < 0 || step >= h->dbg_S) return fail(WRNN_ERR_INVALID, "step " + std::to_string(step) + " was not recorded");
+    if (row < 0 || row >= h->last_B) return fail(WRNN_ERR_INVALID, "row out of range");
+    const int n = h->n_classes;
+    if (capacity < (size_t)n) return fail(WRNN_ERR_CAPACITY, "logit capacity");
+    HIPC(hipMemcpy(out, h->dbg.out + ((size_t)k * h->dbg_rows + row) * n, n * sizeof(float),
+                   hipMemcpyDeviceToHost));
     return WRNN_OK;
 }
 

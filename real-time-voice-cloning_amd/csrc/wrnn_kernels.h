@@ -73,6 +73,15 @@ struct StageArgs {
 constexpr int kMaxStampWG = 2048;  // workgroups recorded per timed launch
 constexpr int kStampEvery = 8;     // timed steps: t % kStampEvery == 0
 
+// Logit capture for the teacher-forced gate (wrnn_set_debug_steps / wrnn_debug_logits): the
+// pre-sampling logits (last linear layer + bias, before softmax / noise) of every row at up to
+// kDbgSteps chosen steps. Off (out == nullptr) in production: one uniform branch per step.
+constexpr int kDbgSteps = 8;
+struct DbgLogits {
+    float* out;             // [kDbgSteps][B][n_classes]
+    const int* map;         // [S]: slot of step t in `out`, or -1
+};
+
 struct SampleArgs {
     int t;          // step whose logits are sampled; -1 = initial GRU1 only (x = 0)
     int S, nrows, n_classes, mode, H;
@@ -91,6 +100,7 @@ struct SampleArgs {
     const RowInfo* rows;
     uint32_t k0, k1;       // Philox key (MOL draws in-kernel)
     uint32_t* phases;      // optional diagnostic: workgroup w stores 6 stamps at [8w + i]
+    DbgLogits dbg;         // rows indexed as in `logits` (the call's row space)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -174,6 +184,11 @@ constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
 enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WORDS = 16 };
 // progress cadence of the reference's callback (fatchord_version.py:234: i % 100 == 0)
 constexpr int kProgressEvery = 100;
+// host-mapped abort request word, kAbortWord words past the progress word (a cache line of its
+// own): set by the host when the progress callback aborts (persist_common.h p_abort)
+constexpr int kAbortWord = 16;
+// PC_ERR codes: 1 registration timeout, 2 exchange timeout, 3 not spread 32 per XCD,
+// 4 aborted by the host (progress callback)
 
 struct PersistArgs {
     unsigned* ctl;          // PC_WORDS control words
@@ -221,6 +236,7 @@ struct PersistArgs {
     // wide-row launches (kernels_persist_wide.hip): MFMA A-operand weight images
     const float4* wwide;    // [kPM][8 waves][40 float4][64 lanes]
     const float4* wwide_lds;// [kPM][2 tiles][8][4][64] (W_hh2 z, n)
+    DbgLogits dbg;
 };
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
@@ -277,6 +293,7 @@ struct PersistRRArgs {
     uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
     unsigned* progress;     // as PersistArgs
     int prog_base;
+    DbgLogits dbg;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
@@ -313,6 +330,7 @@ struct PersistGenArgs {
     unsigned* progress;     // as PersistArgs
     uint32_t k0, k1;        // Philox key (BETA draws in-kernel)
     int prog_base;
+    DbgLogits dbg;
 };
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s);

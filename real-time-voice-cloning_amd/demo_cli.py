@@ -149,14 +149,18 @@ def main():
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         # 3. vocoder: all of this rank's mels as one batch of fold rows (infer_waveform semantics)
+        # utterance i draws noise stream (base + i) on whichever rank runs it, so the vocoder
+        # output does not depend on the number of GPUs
         wavs = []
+        model = vocoder.get_model()
+        base = model.get_stream()
         if specs:
-            model = vocoder.get_model()
             hpv = hparams_for(model.model_type)
             mels = [torch.from_numpy(np.ascontiguousarray(s / sp.max_abs_value, dtype=np.float32)).to(dev)
                     for s in specs]
             wavs = model.generate_batch(mels, True, hpv.gen_target, hpv.gen_overlap, hpv.mu_law,
-                                        sp.preemphasize)
+                                        sp.preemphasize, streams=[base + i for i in mine])
+        model.set_stream(base + args.utterances)
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         # 4. post: pad 1 s (demo_cli.py:197), trim / normalise like the reference

@@ -38,7 +38,8 @@ EXPORTED = [
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
-    'wrnn_debug_beta', 'wrnn_plan_info', 'wrnn_debug_p1',
+    'wrnn_debug_beta', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
+    'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits',
 ]
 
 
@@ -77,13 +78,17 @@ def load_library(path=None):
             f'{LIB_NAME} not found at {path}: build it with `make -C '
             f'real-time-voice-cloning_amd/csrc` or __graft_entry__.build(); the MI355X vocoder '
             f'has no CPU fallback')
-    try:
-        # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7
-        # must be loaded first so this library binds to it (same SONAME) instead of pulling
-        # in /opt/rocm's copy, after which torch.cuda cannot initialise.
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # WRNN_HOST_ONLY=1: a host-only build of the library (the sanitizer build of `make asan`,
+    # tests/test_sanitizers.py) -- no HIP runtime to bind, only the host entry points exist
+    host_only = os.environ.get('WRNN_HOST_ONLY') == '1'
+    if not host_only:
+        try:
+            # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7
+            # must be loaded first so this library binds to it (same SONAME) instead of pulling
+            # in /opt/rocm's copy, after which torch.cuda cannot initialise.
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = ctypes.CDLL(path)
     P = ctypes.POINTER
     c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
@@ -100,6 +105,8 @@ def load_library(path=None):
         'wrnn_load_bin': (c_int, [c_void_p, ctypes.c_char_p, c_size_t]),
         'wrnn_set_seed': (c_int, [c_void_p, ctypes.c_uint64]),
         'wrnn_set_stream': (c_int, [c_void_p, ctypes.c_uint32]),
+        'wrnn_get_stream': (c_int, [c_void_p, P(ctypes.c_uint32)]),
+        'wrnn_set_utt_streams': (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
         'wrnn_fold_shape': (c_int, [c_int, c_int, c_int, c_int, c_int, P(c_int), P(c_int)]),
         'wrnn_generate': (c_int, [c_void_p, P(ctypes.c_float), c_int, c_int, c_int, c_int,
                                   P(ctypes.c_int16), P(ctypes.c_float), c_size_t, P(c_int),
@@ -129,8 +136,12 @@ def load_library(path=None):
         'wrnn_debug_upsample': (c_int, [c_void_p, P(ctypes.c_float), c_size_t,
                                         P(ctypes.c_float), c_size_t]),
         'wrnn_debug_p1': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
+        'wrnn_set_debug_steps': (c_int, [c_void_p, P(c_int), c_int]),
+        'wrnn_debug_logits': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
     }
     for name, (res, args) in sig.items():
+        if host_only and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

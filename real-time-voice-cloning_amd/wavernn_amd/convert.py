@@ -58,19 +58,27 @@ class _Writer:
     def raw(self, fmt, *v):
         self.f.write(struct.pack(fmt, *v))
 
-    def arr(self, a):
+    def arr(self, a, name=''):
         a = _np(a)
         if self.el == 2:
-            a = a.astype(np.float16)
+            with np.errstate(over='ignore'):
+                h = a.astype(np.float16)
+            # a finite value past the fp16 range would be written as inf: refuse the file
+            bad = np.isfinite(a) & ~np.isfinite(h)
+            if bad.any():
+                raise ValueError(f'{name or "array"}: {int(bad.sum())} value(s) outside the fp16 range '
+                                 f'(|x| > 65504, e.g. {float(a[bad][0])}); write this model with '
+                                 f'el_size=4')
+            a = h
         self.f.write(a.tobytes(order='C'))
 
     def layer(self, kind, name):
         self.raw('@i64s', LAYER_IDS[kind], name.encode()[:64])
 
-    def compressed(self, W):
+    def compressed(self, W, name=''):
         w, idx = compress(W)
         self.raw('@i', w.size)
-        self.arr(w)
+        self.arr(w, name)
         self.raw('@i', idx.size)
         self.f.write(idx.tobytes(order='C'))
 
@@ -79,23 +87,23 @@ class _Writer:
         out_ch, in_ch, k = W.shape
         self.layer('Conv1d', 'Conv1d')
         self.raw('@iiiii', self.el, int(bias), in_ch, out_ch, k)
-        self.arr(W)
+        self.arr(W, p + '.weight')
         if bias:
-            self.arr(sd[p + '.bias'])
+            self.arr(sd[p + '.bias'], p + '.bias')
 
     def batchnorm(self, sd, p, eps=1e-5):
         w = _np(sd[p + '.weight'])
         self.layer('BatchNorm1d', 'BatchNorm1d')
         self.raw('@iif', self.el, w.size, eps)
         for f in ('weight', 'bias', 'running_mean', 'running_var'):
-            self.arr(sd[f'{p}.{f}'])
+            self.arr(sd[f'{p}.{f}'], f'{p}.{f}')
 
     def linear(self, sd, p):
         W = _np(sd[p + '.weight'])
         self.layer('Linear', 'Linear')
         self.raw('@iii', self.el, W.shape[0], W.shape[1])
-        self.compressed(W)
-        self.arr(sd[p + '.bias'])
+        self.compressed(W, p + '.weight')
+        self.arr(sd[p + '.bias'], p + '.bias')
 
     def gru(self, sd, p):
         wih, whh = _np(sd[p + '.weight_ih_l0']), _np(sd[p + '.weight_hh_l0'])
@@ -104,9 +112,9 @@ class _Writer:
         self.layer('GRU', 'GRU')
         self.raw('@iii', self.el, H, wih.shape[1])
         for W in (*np.vsplit(wih, 3), *np.vsplit(whh, 3)):
-            self.compressed(W)
+            self.compressed(W, p + '.weight')
         for b in (*np.split(bih, 3), *np.split(bhh, 3)):
-            self.arr(b)
+            self.arr(b, p + '.bias')
 
     def stretch(self, x, y):
         self.layer('Stretch2d', 'Stretch2d')
@@ -137,7 +145,7 @@ def write_bin(f, state_dict, hp, model_type, el_size=EL_SIZE):
         k = _np(sd[f'upsample.up_layers.{2 * j + 1}.weight']).reshape(-1)
         w.layer('Conv2d', 'Conv2d')
         w.raw('@ii', w.el, k.size)
-        w.arr(k)
+        w.arr(k, f'upsample.up_layers.{2 * j + 1}.weight')
     w.linear(sd, 'I')
     if model_type == MODEL_TYPE_FATCHORD:
         grus, fcs = ('rnn1', 'rnn2'), ('fc1', 'fc2', 'fc3')

@@ -172,6 +172,21 @@ class WaveRNN:
     def set_stream(self, stream):
         _abi.check(self._lib.wrnn_set_stream(self._h, ctypes.c_uint32(int(stream))))
 
+    def get_stream(self):
+        """Noise stream the next call's first utterance will use."""
+        s = ctypes.c_uint32()
+        _abi.check(self._lib.wrnn_get_stream(self._h, ctypes.byref(s)))
+        return s.value
+
+    def _set_utt_streams(self, streams, n_utts):
+        if streams is None:
+            return
+        streams = [int(s) for s in streams]
+        if len(streams) != n_utts:
+            raise ValueError(f'{len(streams)} streams for {n_utts} utterances')
+        arr = (ctypes.c_uint32 * len(streams))(*streams)
+        _abi.check(self._lib.wrnn_set_utt_streams(self._h, arr, len(streams)))
+
     def fold_shape(self, n_frames, batched, target, overlap):
         b, s = ctypes.c_int(), ctypes.c_int()
         _abi.check(self._lib.wrnn_fold_shape(int(n_frames), self.hop_length, int(bool(batched)),
@@ -261,6 +276,22 @@ class WaveRNN:
                                            out.size))
         return out
 
+    def set_debug_steps(self, steps):
+        """Record the pre-sampling logits of every fold row at these steps (<= 8) in later
+        calls; [] / None turns recording off (wrnn_set_debug_steps)."""
+        steps = [int(s) for s in (steps or [])]
+        arr = (ctypes.c_int * max(1, len(steps)))(*steps)
+        _abi.check(self._lib.wrnn_set_debug_steps(self._h, arr, len(steps)))
+
+    def debug_logits(self, step, rows):
+        """Logits of the last call at a recorded step: (len(rows), n_classes) float32."""
+        out = np.empty((len(rows), self.n_classes), dtype=np.float32)
+        for i, r in enumerate(rows):
+            _abi.check(self._lib.wrnn_debug_logits(
+                self._h, int(step), int(r), out[i].ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                self.n_classes))
+        return out
+
     def gen_display(self, i, seq_len, b_size, gen_rate):
         pbar = _progbar(i, seq_len)
         msg = f'| {pbar} {i*b_size}/{seq_len*b_size} | Batch Size: {b_size} | Gen Rate: {gen_rate:.1f}kHz | '
@@ -297,12 +328,14 @@ class WaveRNN:
             samples = labels_to_samples(labels, self.n_classes)
         return labels, samples, B, S
 
-    def generate_batch_device(self, mels_dev, batched, target, overlap, progress_callback=None):
+    def generate_batch_device(self, mels_dev, batched, target, overlap, progress_callback=None,
+                              streams=None):
         """Several utterances as one batch of fold rows, inputs resident in HBM.
 
         ``mels_dev``: list of torch CUDA float32 tensors (feat_dims, T_u) on this model's device
         (already normalised). Returns (out_dev, row_offset, S): ``out_dev`` is a torch CUDA
-        tensor (rows, S) -- int16 labels (RAW) or float32 samples (MOL).
+        tensor (rows, S) -- int16 labels (RAW) or float32 samples (MOL). ``streams``: explicit
+        noise stream per utterance (default: the handle's counter + u; wrnn_set_utt_streams).
         """
         import torch
         if not self._loaded:
@@ -331,6 +364,7 @@ class WaveRNN:
         cfn, cb_ref = _wrap_callback(progress_callback)
         torch.cuda.current_stream(dev).synchronize()
         fb0 = self.fallback_info()[0]
+        self._set_utt_streams(streams, n)
         rc = self._lib.wrnn_generate_batch_device(
             self._h, n, ptrs, frames, int(bool(batched)), int(target or 0), int(overlap or 0),
             lab_p, smp_p, rows * S, roff, ctypes.byref(s_out), cfn, None)
@@ -341,11 +375,11 @@ class WaveRNN:
         return out, list(roff), S
 
     def generate_batch(self, mels_dev, batched, target, overlap, mu_law, apply_preemphasis,
-                       progress_callback=None):
+                       progress_callback=None, streams=None):
         """generate() for several device-resident mels; returns a list of f64 waveforms."""
         mu_law = mu_law if self.mode == 'RAW' else False
         out, roff, S = self.generate_batch_device(mels_dev, batched, target, overlap,
-                                                  progress_callback)
+                                                  progress_callback, streams=streams)
         host = out.cpu().numpy()
         self.last_batch_rows, self.last_batch_offsets = host, roff
         return [self.postprocess_rows(host[roff[u]:roff[u + 1]], int(m.shape[-1]), batched,

@@ -33,7 +33,16 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _hp(mode):
+    from wavernn_amd.hparams import wavernn_fatchord
+    return wavernn_fatchord.copy(bits=9, mode=mode)
+
+
+FRAMES = {'RAW': [22, 30, 25], 'MOL': [24, 21]}
+STREAM_BASE = 7  # the callers' stream counter before the call (bench: model.get_stream())
+
+
+def _worker(rank, world, port, q, mode):
     import sys
     import torch
     import torch.distributed as dist
@@ -48,24 +57,33 @@ def _worker(rank, world, port, q):
     from wavernn_amd import _abi
     from wavernn_amd.audio import postprocess
     from wavernn_amd.distributed import infer_waveforms
-    from wavernn_amd.hparams import wavernn_fatchord
     from wavernn_amd.synth import synth_state_dict, synth_mel
-    hp = wavernn_fatchord.copy(bits=9)
+    hp = _hp(mode)
     sd = synth_state_dict(hp, 'fatchord-wavernn', seed=1)
-    mels = [synth_mel(T, seed=10 + i) for i, T in enumerate([22, 30, 25])]
+    mels = [synth_mel(T, seed=10 + i) for i, T in enumerate(FRAMES[mode])]
     lib = _abi.load_library()
+    raw = mode == 'RAW'
+    ran = []
 
-    def rows_fn(ms):
+    def rows_fn(ms, streams):
+        # one stream per utterance of the GLOBAL list, as WaveRNN.generate_batch_device gets it
+        ran.extend(streams)
         outs = [oracle_infer_waveform(sd, hp, 'fatchord-wavernn', m, target=400, overlap=50,
-                                      seed=5, stream=0, post=False)['labels'] for m in ms]
+                                      seed=5, stream=s, post=False)['labels' if raw else 'samples']
+                for m, s in zip(ms, streams)]
         roff = np.cumsum([0] + [o.shape[0] for o in outs]).tolist()
         return torch.from_numpy(np.concatenate(outs)), roff
 
     def post_fn(rows, n_frames):
-        smp = (np.float32(2) * rows.astype(np.float32)) / np.float32(511.) - np.float32(1.)
-        return postprocess(smp, True, 400, 50, True, True, 512, (n_frames - 1) * 200, 200,
-                           labels=rows, lib=lib)
-    wavs = infer_waveforms(mels, rows_fn, post_fn, 400, 50, seq_len=500)
+        if raw:
+            smp = (np.float32(2) * rows.astype(np.float32)) / np.float32(511.) - np.float32(1.)
+            return postprocess(smp, True, 400, 50, True, True, 512, (n_frames - 1) * 200, 200,
+                               labels=rows, lib=lib)
+        return postprocess(rows, True, 400, 50, False, True, 30, (n_frames - 1) * 200, 200,
+                           lib=lib)
+    wavs = infer_waveforms(mels, rows_fn, post_fn, 400, 50, seq_len=500,
+                           stream_base=STREAM_BASE, dtype=torch.int16 if raw else torch.float32)
+    q.put((rank, sorted(ran)))
     if rank == 0:
         q.put([w.tolist() for w in wavs])
     else:
@@ -73,23 +91,57 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gather_equals_single_process():
-    from oracle.wavernn_oracle import oracle_infer_waveform
-    from wavernn_amd.hparams import wavernn_fatchord
-    from wavernn_amd.synth import synth_state_dict, synth_mel
+def _run(world, mode):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    streams, got = {}, None
+    for _ in range(world + 1):
+        item = q.get(timeout=300)
+        if isinstance(item, tuple):
+            streams[item[0]] = item[1]
+        else:
+            got = item
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    hp = wavernn_fatchord.copy(bits=9)
+    return streams, got
+
+
+def _single_process(mode):
+    from oracle.wavernn_oracle import oracle_infer_waveform
+    from wavernn_amd.synth import synth_state_dict, synth_mel
+    hp = _hp(mode)
     sd = synth_state_dict(hp, 'fatchord-wavernn', seed=1)
-    for i, T in enumerate([22, 30, 25]):
-        ref = oracle_infer_waveform(sd, hp, 'fatchord-wavernn', synth_mel(T, seed=10 + i),
-                                    target=400, overlap=50, seed=5, stream=0)['wav']
-        assert np.array_equal(np.asarray(got[i]), ref)
+    return [oracle_infer_waveform(sd, hp, 'fatchord-wavernn', synth_mel(T, seed=10 + i),
+                                  target=400, overlap=50, seed=5, stream=STREAM_BASE + i)['wav']
+            for i, T in enumerate(FRAMES[mode])]
+
+
+def test_two_rank_gather_equals_single_process():
+    """N = 2 == N = 1 bit for bit: utterance i draws stream base + i on whichever rank runs it
+    (world-size invariant output), and every stream is used exactly once."""
+    streams, got = _run(2, 'RAW')
+    ref = _single_process('RAW')
+    n = len(FRAMES['RAW'])
+    assert sorted(s for r in streams.values() for s in r) == [STREAM_BASE + i for i in range(n)]
+    for i in range(n):
+        assert np.array_equal(np.asarray(got[i]), ref[i])
+
+
+def test_three_ranks_two_mol_utterances_empty_shard():
+    """More ranks than utterances: the empty rank still gathers a buffer of the MOL rows'
+    dtype (float32), so the gather matches the others' byte size; output == one process."""
+    streams, got = _run(3, 'MOL')
+    assert [] in streams.values()
+    ref = _single_process('MOL')
+    for i in range(len(FRAMES['MOL'])):
+        assert np.array_equal(np.asarray(got[i]), ref[i])
+
+
+def test_empty_utterance_list():
+    from wavernn_amd.distributed import infer_waveforms
+    assert infer_waveforms([], None, None, 400, 50, seq_len=500) == []

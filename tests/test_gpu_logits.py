@@ -1,0 +1,109 @@
+"""Teacher-forced logit gate (SURVEY §7 "Hard parts" iii): the HIP kernels'
+pre-sampling logits against the ones the reference itself produced.
+
+Every golden fixture stores the reference's logits at recorded steps (tests/golden/gen_golden.py,
+captured from fatchord_version.py:213 / runtimeracer_version.py:270 / geneing_version.py). The
+GPU call runs the same (weights, mel, noise) and, since its labels / samples equal the
+reference's (test_gpu_parity.py), its recurrence is teacher-forced by the reference's own
+history: the logits it records at those steps (wrnn_set_debug_steps / wrnn_debug_logits,
+written by the kernel that runs the call) are comparable element for element.
+
+Bar: max |logit_gpu - logit_ref| <= 1e-5 on every fixture, every engine and launch kind. The
+test also reports the smallest top-2 gap of the recorded steps' Gumbel-max decisions, i.e. how
+far each decision was from flipping, next to the error.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_case, golden_meta
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_ABS_TOL = 1e-5
+
+CASES = [(k, e) for k in golden_meta() for e in ('persist', 'chain')]
+# the wide MFMA launch (kernels_persist_wide.hip) on the fatchord RAW <= 512-class fixtures
+WIDE = ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny', 'fatchord_raw9_config1']
+
+
+def _run(name, engine, wide=False, monkeypatch=None):
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, gold = golden_case(name)
+    if wide:
+        monkeypatch.setenv('WRNN_PERSIST_WIDE', '1')
+    m, hp, sd = make_model(meta)
+    m.set_engine(engine)
+    steps = [int(s) for s in gold['logits_steps']]
+    m.set_debug_steps(steps)
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    m.enable_stage_timing(True)
+    m.generate(mel[None], meta['batched'], meta['target'], meta['overlap'], hp.mu_law,
+               sp.preemphasize, progress_callback=lambda *a: None)
+    assert m.last_engine() == engine
+    if wide:
+        assert [s[0] for s in m.stage_info()] == ['persist_wide']
+    rows = range(meta['num_folds'])
+    got = np.stack([m.debug_logits(s, rows) for s in steps])
+    return meta, gold, m, got
+
+
+def _gap(meta, gold, got):
+    """Smallest top-2 gap (log domain) of the categorical decisions at the recorded steps:
+    argmax_k (l_k - log q_k) with the contract's noise (0 for continuous heads)."""
+    if meta['mode'] == 'MOL' or gold['logits'].shape[-1] <= 2:
+        return None
+    from oracle import philox
+    gaps = []
+    for i, s in enumerate(gold['logits_steps']):
+        q = philox.raw_exp_noise(meta['noise_seed'], 0, [int(s)], np.arange(meta['num_folds']),
+                                 gold['logits'].shape[-1])[0].astype(np.float64)
+        v = gold['logits'][i].astype(np.float64) - np.log(q)
+        v.sort(axis=-1)
+        gaps.append(float((v[:, -1] - v[:, -2]).min()))
+    return min(gaps)
+
+
+def _check(name, meta, gold, got):
+    ref = gold['logits']
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert np.isfinite(got).all(), f'{name}: a recorded logit was never written'
+    err = float(np.abs(got.astype(np.float64) - ref.astype(np.float64)).max())
+    gap = _gap(meta, gold, got)
+    print(f'{name}: max |dlogit| {err:.3g} (|logit| <= {np.abs(ref).max():.3g}), '
+          f'min top-2 gap {gap}')
+    assert err <= LOGIT_ABS_TOL, f'{name}: max logit error {err}'
+    if gap is not None:
+        assert gap > 2 * err  # every recorded decision is farther from a flip than the error
+
+
+@pytest.mark.parametrize('name,engine', CASES)
+def test_logits_match_reference(name, engine):
+    meta, gold, m, got = _run(name, engine)
+    _check(name, meta, gold, got)
+
+
+@pytest.mark.parametrize('name', WIDE)
+def test_wide_logits_match_reference(name, monkeypatch):
+    meta, gold, m, got = _run(name, 'persist', wide=True, monkeypatch=monkeypatch)
+    _check(name, meta, gold, got)
+
+
+def test_capture_off_and_unrecorded_step():
+    """Recording is per handle and off by default; an unrecorded step is refused."""
+    meta, gold, m, got = _run('fatchord_raw9_tiny', 'persist')
+    with pytest.raises(ValueError, match='not recorded'):
+        m.debug_logits(3, [0])
+    m.set_debug_steps([])
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+    m.set_seed(meta['noise_seed'])
+    wav = m.generate(mel[None], meta['batched'], meta['target'], meta['overlap'], True, True,
+                     progress_callback=lambda *a: None)
+    assert np.array_equal(wav, gold['wav'])
+    with pytest.raises(ValueError, match='recorded no logits'):
+        m.debug_logits(0, [0])
