@@ -99,7 +99,7 @@ def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False):
     return hops * HANDOFF_US + flop / CU_FP32_FLOP_PER_US, hops
 
 
-def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0):
+def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0, **kw):
     import torch
     from oracle.wavernn_oracle import OracleWaveRNN
     torch.set_num_threads(threads)
@@ -107,7 +107,7 @@ def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0):
     m = torch.from_numpy(mel[None] / 4.0)
     t0 = time.perf_counter()
     r = o.generate(m, True, args.target, args.overlap, hp.mu_law, True, max_steps=max_steps,
-                   seed=seed, stream=stream)
+                   seed=seed, stream=stream, **kw)
     r['t_wall'] = time.perf_counter() - t0
     return r
 
@@ -157,6 +157,37 @@ def _parity(r, gpu_rows, gpu_wav, seed, stream):
         parity['wave_rms'] = float(np.sqrt(np.mean((gpu_wav - r['wav']) ** 2)))
         parity['tolerance'] = 1e-4
     return parity
+
+
+def logit_gate(args, sd, hp, model, mel_dev, mel, gpu_rows, seed, stream):
+    """Teacher-forced logit gate on the timed configuration (SURVEY §7 hard parts iii): the
+    same call re-run with the kernels recording their pre-sampling logits at 6 steps (same seed
+    and stream, so also a determinism check of the timed call's labels), against the oracle's
+    logits at those steps; and the oracle's smallest top-1 / top-2 decision gap over EVERY
+    (step, row) draw of the call -- how close the closest draw came to flipping."""
+    import numpy as np
+    import torch
+    S = gpu_rows.shape[1]
+    steps = sorted({0, 1, S // 4, S // 2, 3 * S // 4, S - 1})
+    model.set_debug_steps(steps)
+    try:
+        rows, roff, _ = model.generate_batch_device([mel_dev], True, args.target, args.overlap,
+                                                    streams=[stream])
+        rerun = rows.cpu().numpy()[roff[0]:roff[1]]
+        got = np.stack([model.debug_logits(t, range(rerun.shape[0])) for t in steps])
+    finally:
+        model.set_debug_steps([])
+    r = _oracle_run(args, sd, hp, mel, torch.get_num_threads(), seed=seed, stream=stream,
+                    record_logits=set(steps), track_margin=model.categorical, post=False)
+    ref = np.stack([r['logits'][t] for t in steps])
+    out = {'steps': steps, 'max_abs_logit_err': float(np.abs(got.astype(np.float64) - ref).max()),
+           'max_abs_logit': float(np.abs(ref).max()), 'tolerance': 1e-5,
+           'rerun_identical': bool(np.array_equal(rerun, gpu_rows))}
+    if 'margin' in r:
+        out['min_top2_gap'] = r['margin']['min_gap']
+        out['min_top2_gap_at'] = [r['margin']['step'], r['margin']['row']]
+        out['min_top2_gap_over'] = f"{r['B']} rows x {r['S']} steps (log(p/q) top-1 - top-2)"
+    return out
 
 
 def parity_check(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
@@ -377,6 +408,8 @@ def main():
                     'progress callback at i % 100 == 0 (reference cadence)'}
         result['cpu_baseline'], result['parity'] = cpu_baseline(args, sd, hp, mels_host[0],
                                                                 gpu_rows, wavs[0], seed, stream)
+        result['parity']['logits'] = logit_gate(args, sd, hp, model, mels[0], mels_host[0],
+                                                gpu_rows, seed, stream)
     elif rank == 0 and world > 1 and args.cpu_seconds > 0:
         # N > 1: one utterance of the LAST rank's shard, gathered over RCCL, against the oracle
         # on its global stream (world-size invariance: the same labels as at N = 1)

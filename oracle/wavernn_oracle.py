@@ -221,12 +221,18 @@ class OracleWaveRNN:
         return logits, (h1, h2, h3, h4)
 
     # --- samplers --------------------------------------------------------------------
-    def sample_raw(self, logits, q):
-        """fatchord_version.py:225-228 with Categorical.sample() == argmax(probs / q)."""
+    def sample_raw(self, logits, q, gaps=None):
+        """fatchord_version.py:225-228 with Categorical.sample() == argmax(probs / q).
+        ``gaps``: a list that receives, per row, the decision's top-1 / top-2 gap
+        log(r1) - log(r2) of the fp32 ratios r = probs / q (how far the draw was from a flip)."""
         posterior = F.softmax(logits, dim=1)
         probs = posterior / posterior.sum(-1, keepdim=True)   # Categorical.__init__
-        k = torch.argmax(probs / q, dim=-1)                   # multinomial fast path
+        ratio = probs / q
+        k = torch.argmax(ratio, dim=-1)                       # multinomial fast path
         sample = 2 * k.float() / (self.n_classes - 1.) - 1.
+        if gaps is not None:
+            top = torch.topk(ratio, 2, dim=-1).values.double().numpy()
+            gaps.append(np.log(top[:, 0]) - np.log(top[:, 1]))
         return k, sample
 
     @staticmethod
@@ -263,7 +269,7 @@ class OracleWaveRNN:
 
     def generate(self, mels, batched, target, overlap, mu_law, apply_preemphasis, seed=0,
                  stream=0, max_steps=None, progress_callback=None, record_logits=None,
-                 post=True):
+                 post=True, track_margin=False):
         """Restates generate(); returns a dict with 'wav' and per-row outputs.
 
         ``mels``: torch (1, n_mels, T) float32, already divided by max_abs_value.
@@ -272,6 +278,8 @@ class OracleWaveRNN:
         ``post=False``: rows only, no post-processing ('wav' None) -- mels shorter than the
         20-hop tail fade have rows but no waveform (the reference raises there, :253-255).
         ``record_logits``: optional list of step indices whose logits are returned.
+        ``track_margin``: RAW only -- 'margin' = the smallest top-1 / top-2 gap (log of the fp32
+        probs / q ratios) over every (step, row) decision, with its step and row.
         """
         mu_law = mu_law if self.mode == 'RAW' else False  # geneing BITS: no mu-law (:158)
         start = time.time()
@@ -291,6 +299,7 @@ class OracleWaveRNN:
             labels = np.zeros((b_size, n_steps), dtype=np.int16)
             samples = []
             logits_rec = {}
+            margin = [math.inf, -1, -1]
             t0 = time.time()
             for i in range(n_steps):
                 m_t = mels[:, i, :]
@@ -315,7 +324,12 @@ class OracleWaveRNN:
                 else:
                     q = torch.from_numpy(philox.raw_exp_noise(seed, stream, [i], rows,
                                                               self.n_classes)[0])
-                    k, sample = self.sample_raw(logits, q)
+                    g = [] if track_margin else None
+                    k, sample = self.sample_raw(logits, q, g)
+                    if g:
+                        j = int(np.argmin(g[0]))
+                        if g[0][j] < margin[0]:
+                            margin[:] = [float(g[0][j]), i, j]
                     labels[:, i] = k.numpy().astype(np.int16)
                     samples.append(sample)
                     x = sample.unsqueeze(-1)
@@ -328,6 +342,8 @@ class OracleWaveRNN:
         output = torch.stack(samples).transpose(0, 1)
         out['samples'] = output.numpy().copy()
         out['logits'] = logits_rec
+        if track_margin and margin[1] >= 0:
+            out['margin'] = {'min_gap': margin[0], 'step': margin[1], 'row': margin[2]}
         if n_steps < seq_len or not post:
             out['wav'] = None
             return out

@@ -13,12 +13,8 @@ namespace wrnn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-#ifndef WRNN_GEMM_WPE
-#define WRNN_GEMM_WPE 3  // waves per SIMD the GEMM is compiled for
-#endif
-#ifndef WRNN_GEMM_WIDE_NT
-#define WRNN_GEMM_WIDE_NT 4  // 64-wide column tiles per workgroup for wide outputs (P1)
-#endif
+constexpr int kGemmWavesPerSimd = 3;  // waves per SIMD the GEMM is compiled for
+constexpr int kGemmWideNT = 4;        // 64-wide column tiles per workgroup for wide outputs (P1)
 
 // A(m, .) of one row as two strided segments: k < ksplit reads p0[o0 + k * s0], the rest
 // p1[o1 + k * s1] (o1 may be negative: it is only ever used with k >= ksplit). The row's
@@ -104,7 +100,7 @@ __device__ __forceinline__ void store_ep(const GemmEp& e, int m, int n, float ac
 // launch-latency-bound MelResNet GEMMs (two to seven global round trips per tile instead of 8-25;
 // the k order of the MFMA chain is the same, so are the results).
 template <int NT, int AK, int BK>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WRNN_GEMM_WPE))) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kGemmWavesPerSimd))) void k_gemm(int M, int N, int K, GemmA A, GemmB B,
                                                    GemmEp E) {
     __shared__ float As[BK][64];
     __shared__ float Bs[BK][64 * NT];
@@ -208,8 +204,8 @@ hipError_t launch_gemm(int M, int N, int K, const GemmA& a, const GemmB& b, cons
     if (a.kind < 0 || a.kind > 2) return hipErrorInvalidValue;
     const int m_tiles8 = ((M + 63) / 64 + 7) / 8 * 8;  // k_gemm's XCD-aware tile order
     if (N >= 1024)  // wide outputs (P1: 3H / 4H columns): 4 column tiles per workgroup
-        launch_nt<WRNN_GEMM_WIDE_NT, 16>(
-            dim3(m_tiles8 * ((N + 64 * WRNN_GEMM_WIDE_NT - 1) / (64 * WRNN_GEMM_WIDE_NT))), M, N,
+        launch_nt<kGemmWideNT, 16>(
+            dim3(m_tiles8 * ((N + 64 * kGemmWideNT - 1) / (64 * kGemmWideNT))), M, N,
             K, a, b, e, s);
     else if ((M + 63) / 64 * ((N + 63) / 64) <= 256 && K >= 64)
         // fewer tiles than CUs (MelResNet: M = 128 channels, N = frames): latency-bound, so

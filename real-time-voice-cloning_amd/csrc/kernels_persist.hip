@@ -49,7 +49,7 @@ constexpr int XB_A_SZ = kPNR * 5 * kPH * 2;
 constexpr int XB_B = XB_A + 2 * XB_A_SZ;
 constexpr int XB_C = XB_B + kPNR * kPH * 2;
 constexpr int XB_D = XB_C + kPNR * kPH * 2;
-// RAW candidates [slot][r][value, tag] or, per wave (WRNN_WAVE_CAND), [slot][r][wave 0-3][value, tag]
+// RAW candidates [slot][r][value, tag] (the area is sized for 4 per slot and row)
 constexpr int XB_D_LOG = kPM * kPNR * 4 * 2;
 constexpr int XB_D_SZ = XB_D_LOG + kPNR * 64;      // MOL logits [r][64]
 constexpr int XB_G = XB_D + XB_D_SZ;              // gh1 [parity][r][unit] (r, z, n, -) float4
@@ -66,7 +66,7 @@ constexpr int L_XH2 = L_X1 + kPNR * kPH;            // [kPNR][512] h2 (staged at
 constexpr int L_RED = L_XH2 + kPNR * kPH;           // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
-constexpr int L_SINK = L_SX + 14;                   // float2 sink of padding poll lanes
+
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
 constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
@@ -78,12 +78,6 @@ constexpr int L_TOTAL = L_W + 4 * kPLdsW4;
 static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
-#ifndef WRNN_X2_LOCAL
-#define WRNN_X2_LOCAL 1  // hop A carries h2 only; every slot forms x2 = x1 + h2 (see hop A)
-#endif                   // (RAW only: MOL measured 6.28 vs 6.24 us per step with it)
-#ifndef WRNN_X2_LOCAL_MOL
-#define WRNN_X2_LOCAL_MOL 0
-#endif
 
 // P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
 template <int NR, bool FC3R, bool MOL, bool P1R>
@@ -116,12 +110,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // (wave 0) at [24] / [25] give the core clock against the 100 MHz stamps
 #define XSTAMP(i)                                                        \
     if (trace && t == a.phase_t && tid == 0) ph[(i)] = p_now();
-#ifndef WRNN_PQB3  // float4 per row per LDS batch of the 3-gate / 1-gate products
-#define WRNN_PQB3 2
-#endif
-#ifndef WRNN_PQB1
-#define WRNN_PQB1 2
-#endif
+    // float4 per row per LDS batch of the 3-gate / 1-gate products (2 / 2 fastest)
+    constexpr int kPQB3 = 2, kPQB1 = 2;
 #define PSTAMP(i)                                                        \
     if (trace && t == a.phase_t && (tid & 255) == 0) {                   \
         ph[(tid >> 8) * 12 + (i)] = p_now();                             \
@@ -193,12 +183,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // issue theirs after the candidate publish, off the critical path (a wave polls only
     // with no bulk loads in flight: its first poll would wait for all of them).
     constexpr bool EARLY = !FC3R;  // sampling lanes: st = EARLY ? tid - 256 : tid in [0, 32 NR)
-    constexpr bool X2L = MOL ? WRNN_X2_LOCAL_MOL : WRNN_X2_LOCAL;
-#ifndef WRNN_WAVE_CAND
-#define WRNN_WAVE_CAND 0  // A/B: 6.75 vs 6.53 us per C2 step (slower), see DESIGN §3.0
-#endif
-    // RAW candidates per wave of 0-3 ([slot][r][wave]) instead of per slot through LDS
-    constexpr bool WCAND = WRNN_WAVE_CAND && !MOL && !FC3R;
+    // local x2 (RAW): hop A carries h2 only and every slot forms x2 = x1 + h2 itself (see hop
+    // A); MOL publishes x2 (measured 6.28 vs 6.24 us per step with the local form)
+    constexpr bool X2L = !MOL;
     // Loads are unconditional (step indices clamped; past the last step the values go
     // unused): every path to the loop's back edge then consumes them, so the compiler's
     // wait insertion sees no load pending at the top of the step.
@@ -310,7 +297,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // loads of a batch in flight together (one LDS round trip per batch, not per row);
         // each row still accumulates in k order, as a row-outer loop would.
         auto mv3 = [&](const float4* Xs, float& s0, float& s1, float& s2) {
-            constexpr int QB = NR >= 4 ? 1 : WRNN_PQB3;
+            constexpr int QB = NR >= 4 ? 1 : kPQB3;
             v2f acc[NR][3];
 #pragma unroll
             for (int r = 0; r < NR; ++r)
@@ -372,21 +359,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         XSTAMP(30);
         PSTAMP(1);
         // ===== hop A: stage x2 -> X0, h2 -> XH2 (waves 0-3) ======================================
-#ifndef WRNN_H2_LATE
-#define WRNN_H2_LATE 1
-#endif
-        // H2_LATE: hop A waits for x2 only; waves 0-3 fetch h2 (published with x2, needed first
-        // by the off-path W_hh2 h2 of hop B) during stage B, where they are otherwise idle
-        constexpr int NA = WRNN_H2_LATE ? 1 : 2;  // arrays polled in hop A
-        // X2_LOCAL: x1 is the same in every slot (GRU1 runs redundantly), so hop A carries h2
-        // only and each poll lane forms x2 = x1 + h2 of its couples itself -- the producer's own
-        // fp32 add on the same operands (bit-identical x2), one publish instead of two, and no
-        // second poll for h2
-#ifndef WRNN_HOPA_ALL
-#define WRNN_HOPA_ALL 0  // A/B: 6.38 vs 6.28 us per C2 step (slower)
-#endif
-        // HOPA_ALL: x2 polled by all 8 waves (waves 4-7 are done with W_hh1 by then): half the
-        // couples per lane
+        // Late h2: hop A waits for x2 only; waves 0-3 fetch h2 (published with x2, needed first
+        // by the off-path W_hh2 h2 of hop B) during stage B, where they are otherwise idle.
+        // Local x2 (RAW): x1 is the same in every slot (GRU1 runs redundantly), so hop A carries
+        // h2 only and each poll lane forms x2 = x1 + h2 of its couples itself -- the producer's
+        // own fp32 add on the same operands (bit-identical x2), one publish instead of two, and
+        // no second poll for h2. (Polling x2 with all 8 waves measured slower: 6.38 vs 6.28 us.)
         if (X2L) {
             if (wv_lo) {
                 unsigned off[NR];
@@ -407,39 +385,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     *x = v;
                 }
             }
-        } else if (WRNN_H2_LATE && WRNN_HOPA_ALL) {
-            constexpr int TOT = NR * (kPH / 2), MA = (TOT + kPT - 1) / kPT;
-            unsigned off[MA];
-            float2* dst[MA];
-            int tx = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
-            asm volatile("" : "+v"(tx));
+        } else if (wv_lo) {  // x2 -> X0, polling the tagged pairs, one pass
+            unsigned off[NR];
+            float2* dst[NR];
 #pragma unroll
-            for (int m = 0; m < MA; ++m) {
-                const int c = tx + kPT * m;
-                const bool valid = c < TOT;
-                const int cc = valid ? c : c - TOT;  // padding lanes re-poll a valid couple
-                const int r = cc / (kPH / 2), cp = cc % (kPH / 2);
-                off[m] = (unsigned)(r * 5 * kPH + 2 * cp) * 8u;
-                dst[m] = valid ? reinterpret_cast<float2*>(lds + L_X0 + r * kPH) + cp
-                               : reinterpret_cast<float2*>(lds + L_SINK);
+            for (int m = 0; m < NR; ++m) {  // couple tl of row m
+                off[m] = (unsigned)(m * 5 * kPH + 2 * tl) * 8u;
+                dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
             }
-            if (!poll_couples<MA>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
-        } else if (wv_lo) {  // polling the tagged pairs, one pass
-            unsigned off[NA * NR];
-            float2* dst[NA * NR];
-#pragma unroll
-            for (int m = 0; m < NA * NR; ++m) {  // couple tl of (row m / NA, array m % NA)
-                off[m] = (unsigned)(((m / NA) * 5 + (m % NA)) * kPH + 2 * tl) * 8u;
-                dst[m] = reinterpret_cast<float2*>(lds + ((m % NA) ? L_XH2 : L_X0) + (m / NA) * kPH) + tl;
-            }
-            if (!poll_couples<NA * NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+            if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(2);
         // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
         auto mv1 = [&](float bias) {
-            constexpr int QB = NR >= 4 ? 1 : WRNN_PQB1;
+            constexpr int QB = NR >= 4 ? 1 : kPQB1;
             float s0 = 0.f;
             v2f acc[NR];
 #pragma unroll
@@ -471,7 +432,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             // gh1 (hop A) must be in L2 before this wave's y1 can be seen
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
-        } else if (WRNN_H2_LATE && !X2L) {  // h2 -> XH2 (tags stored with x2's: one pass)
+        } else if (!X2L) {  // late h2 -> XH2 (tags stored with x2's: one pass)
             unsigned off[NR];
             float2* dst[NR];
 #pragma unroll
@@ -484,11 +445,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // gh2 = W_hh2 h2 + b_hh2 (next step's GRU2), off the critical path, spread over the
         // exchange waits: rows r % 3 == 0 by waves 0-3 in hop B, r % 3 == 1 by waves 4-7 in hop
         // C, r % 3 == 2 by waves 4-7 in hop D (LDS weights, h2 staged in XH2)
-#ifndef WRNN_HH2_MAP
-#define WRNN_HH2_MAP 0
-#endif
         // window of row r's gh2: 0 hop B (waves 0-3), 1 hop C (waves 4-7), 2 hop D (waves 4-7)
-        auto hh2_win = [](int r) { return WRNN_HH2_MAP ? (r & 1) : r % 3; };
+        auto hh2_win = [](int r) { return r % 3; };
         auto hh2_rows = [&](auto win_c, int ul) {
             constexpr int WIN = decltype(win_c)::value;
             const float4* Wh = reinterpret_cast<const float4*>(lds + L_W) + (size_t)ul * 3 * kPK4;
@@ -650,113 +608,71 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             } else {
                 fc3();
             }
-            // RAW, <= 16 classes per slot (WCAND): every wave of 0-3 publishes the candidate of
-            // its 4 classes per row straight from registers (shuffles over its 4 DPP rows), so
-            // no LDS round trip and no workgroup barrier sit between fc3 and the publish
-            if constexpr (WCAND) {
-                if (wv_lo) {
-                    float bv = -INFINITY;
-                    int bi = 0x7ff;
-                    if (kc < NR && has_cls) {
-                        const float l = p_add(s0, lds[L_BCLS + og]);
-                        bv = p_add(l, pgum);
-                        bi = cls;
-                    }
-#pragma unroll
-                    for (int m = 16; m <= 32; m <<= 1) {  // lanes kc == r of the wave's 4 classes
-                        const float v2 = __shfl_xor(bv, m);
-                        const int k2 = __shfl_xor(bi, m);
-                        if (v2 > bv || (v2 == bv && k2 < bi)) {
-                            bv = v2;
-                            bi = k2;
+            float* red = lds + L_RED;  // [og][r][value, class]
+            if (kc < NR) {
+                float val = -INFINITY;
+                if (has_cls) {
+                    const float l = p_add(s0, lds[L_BCLS + og]);
+                    p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    if (!MOL)
+                        val = p_add(l, pgum);
+                    else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
+                        bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
+                }
+                red[(og * kPNR + kc) * 2] = val;
+                red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
+            }
+            XSTAMP(28);
+            __syncthreads();
+            PSTAMP(11);
+            if (wv_lo) {
+            if (wave == 0) {
+                if (!MOL) {
+                    // slot candidate per row, tagged with the step (no flag, no wait)
+                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
+                    asm volatile("" : "+v"(tt));
+                    if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
+                        const int r = tt >> 4, o = tt & 15;
+                        float bv = -INFINITY;
+                        int bi = 0x7fffffff;
+                        if (r < NR && o < a.cpw) {
+                            bv = red[(o * kPNR + r) * 2];
+                            bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                         }
-                    }
-                    XSTAMP(28);
-                    if (kc < NR && (tid & 48) == 0) {
-                        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
-                        int kx = kc;  // (recomputed per step: hoisted offsets cost registers)
-                        asm volatile("" : "+v"(kx));
-                        __builtin_amdgcn_raw_buffer_store_b64(
-                            (u2v){__float_as_uint(bv), tag_hi | ((unsigned)bi & 0x7ffu)}, xr,
-                            (unsigned)(((w * kPNR + kx) * 4 + wave) * 2) * 4u, XB_D * 4, 0);
-                    }
-                    PSTAMP(11);
-                    if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
-                        gru1_loads();
-                        XSTAMP(27);
-                    }
-                } else if (NR > 2 && !WRNN_HH2_MAP) {
-                    PSTAMP(11);
-                    // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
-                    hh2_rows(std::integral_constant<int, 2>(), og - 16);
-                }
-            } else {
-                float* red = lds + L_RED;  // [og][r][value, class]
-                if (kc < NR) {
-                    float val = -INFINITY;
-                    if (has_cls) {
-                        const float l = p_add(s0, lds[L_BCLS + og]);
-                        p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
-                        if (!MOL)
-                            val = p_add(l, pgum);
-                        else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
-                            bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
-                    }
-                    red[(og * kPNR + kc) * 2] = val;
-                    red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
-                }
-                XSTAMP(28);
-                __syncthreads();
-                PSTAMP(11);
-                if (wv_lo) {
-                if (wave == 0) {
-                    if (!MOL) {
-                        // slot candidate per row, tagged with the step (no flag, no wait)
-                        const unsigned tag_hi = (seq & kTagSeqMask) << 11;
-                        int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
-                        asm volatile("" : "+v"(tt));
-                        if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
-                            const int r = tt >> 4, o = tt & 15;
+                        row16_argmax(bv, bi);
+                        const int rr = r;
+                        if (r < NR && o == 0)
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
+                                (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
+                    } else {
+#pragma unroll
+                        for (int rb = 0; rb < NR; rb += 2) {
+                            const int r = rb + (tt >> 5), o = tt & 31;
                             float bv = -INFINITY;
                             int bi = 0x7fffffff;
                             if (r < NR && o < a.cpw) {
                                 bv = red[(o * kPNR + r) * 2];
                                 bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
                             }
-                            row16_argmax(bv, bi);
+                            half_argmax(bv, bi);
                             const int rr = r;
-                            if (r < NR && o == 0)
+                            if (r < NR && o == 31)
                                 __builtin_amdgcn_raw_buffer_store_b64(
                                     (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
                                     (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
-                        } else {
-    #pragma unroll
-                            for (int rb = 0; rb < NR; rb += 2) {
-                                const int r = rb + (tt >> 5), o = tt & 31;
-                                float bv = -INFINITY;
-                                int bi = 0x7fffffff;
-                                if (r < NR && o < a.cpw) {
-                                    bv = red[(o * kPNR + r) * 2];
-                                    bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
-                                }
-                                half_argmax(bv, bi);
-                                const int rr = r;
-                                if (r < NR && o == 31)
-                                    __builtin_amdgcn_raw_buffer_store_b64(
-                                        (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                        (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
-                            }
                         }
                     }
                 }
-                if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
-                    gru1_loads();
-                    XSTAMP(27);
-                }
-                } else {
-                    // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
-                    if (NR > 2 && !WRNN_HH2_MAP) hh2_rows(std::integral_constant<int, 2>(), og - 16);
-                }
+            }
+            if (EARLY) {  // waves 0-3: GRU1 operands after the candidate publish
+                gru1_loads();
+                XSTAMP(27);
+            }
+            } else {
+                // hop D: W_hh2 h2 rows r % 3 == 2 (waves 4-7, before their candidate poll)
+                if (NR > 2) hh2_rows(std::integral_constant<int, 2>(), og - 16);
             }
         }
         if (FC3R) gru1_loads();
@@ -771,34 +687,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 unsigned n = 0;
                 float bv;
                 int bi;
-                if constexpr (WCAND) {  // the slot's 4 wave candidates: two 16-byte loads
-                    const unsigned off = (unsigned)((o * kPNR + r) * 4 * 2) * 4u;
-                    u4v c = __builtin_amdgcn_raw_buffer_load_b128(xr, off, XB_D * 4, kCpNT);
-                    u4v d = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, XB_D * 4, kCpNT);
-                    while (true) {  // two polls in flight (see poll_couples)
-                        const u4v c1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, XB_D * 4, kCpNT);
-                        const u4v d1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16u, XB_D * 4, kCpNT);
-                        if (__all((c.y >> 11) == want && (c.w >> 11) == want && (d.y >> 11) == want &&
-                                  (d.w >> 11) == want))
-                            break;
-                        c = c1;
-                        d = d1;
-                        if ((++n & 255) == 0) {
-                            if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
-                                if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
-                                lds[L_FAIL] = 1.f;
-                                break;
-                            }
-                        }
-                    }
-                    // waves hold ascending classes: a later wave wins only when strictly larger
-                    bv = __uint_as_float(c.x);
-                    bi = (int)(c.y & 0x7ffu);
-                    const float v1 = __uint_as_float(c.z), v2 = __uint_as_float(d.x), v3 = __uint_as_float(d.z);
-                    if (v1 > bv) { bv = v1; bi = (int)(c.w & 0x7ffu); }
-                    if (v2 > bv) { bv = v2; bi = (int)(d.y & 0x7ffu); }
-                    if (v3 > bv) { bv = v3; bi = (int)(d.w & 0x7ffu); }
-                } else {
+                {
                     const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
                     u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
                     while (true) {  // two polls in flight (see poll_couples)
@@ -960,13 +849,10 @@ hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
 // RAW Gumbel noise g = -log(q), q the contract's Exp(1) variate (philox.h exp1_from_u32, its
 // float64 log kept exact): argmax_k (l_k + g_k) is the decision of argmax_k ((softmax(l)_k / sum)
 // / q_k). The second log runs in fp32 (logf, ~1 ulp: the order of the fp32 rounding the
-// reference's own p / q carries) unless WRNN_GUMBEL_F64 is defined.
+// reference's own p / q carries; both logs in float64 took 0.88 instead of 0.54 ms per C2 call,
+// labels unchanged).
 __device__ __forceinline__ float gumbel_of(uint32_t x) {
-#ifdef WRNN_GUMBEL_F64
-    return (float)(-log((double)exp1_from_u32(x)));
-#else
     return -logf(exp1_from_u32(x));
-#endif
 }
 __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int ng,
                                                 const RowInfo* rows, uint32_t k0, uint32_t k1) {

@@ -20,9 +20,6 @@
 //            published (so no producer can overwrite them first)
 // then, redundantly in every workgroup, the sample and GRU1 of the next step (rank-1 x term).
 #include "wrnn_kernels.h"
-#ifndef WRNN_POLL_ALL_FIRST
-#define WRNN_POLL_ALL_FIRST 1  // first poll pass loads every couple (measured faster here)
-#endif
 #include "persist_common.h"
 #include "philox.h"
 
@@ -77,7 +74,7 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
         off[m] = (unsigned)((r * NPAIR + 2 * cp) * 8);
         d[m] = valid ? reinterpret_cast<float2*>(dst + r * NPAIR) + cp : reinterpret_cast<float2*>(sink);
     }
-    return poll_couples<M>(xr, off, so, seq, d, ctl);
+    return poll_couples<M, true>(xr, off, so, seq, d, ctl);  // first pass loads every couple
 }
 
 }  // namespace

@@ -203,18 +203,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     const bool has_cls = cl < a.cpw && cls < a.n_classes;
     const int j = tid & (RH - 1), hs = tid >> 8;  // GRU1: unit j of rows r = 2 i + hs
     constexpr int NRH = (NR + 1) / 2;
-#ifndef WRNN_RR_H_LATE
-#define WRNN_RR_H_LATE 1
-#endif
-    // H_LATE: each GRU hop waits for x only; idle quads fetch h2 / h3 / h4 in the next stage
+    // late h: each GRU hop waits for x only; idle quads fetch h2 / h3 / h4 in the next stage
     // and the off-path W_hh2 h2 / W_hh3 h3 run one stage later (stages 3 / 4)
-    constexpr bool HL = WRNN_RR_H_LATE;
-#ifndef WRNN_RR_X_LOCAL
-#define WRNN_RR_X_LOCAL 1
-#endif
-    // X_LOCAL (with H_LATE): the GRU hops carry h only and every slot forms x itself
+    constexpr bool HL = true;
+    // local x (with late h): the GRU hops carry h only and every slot forms x itself
     // (x1 is identical everywhere: GRU1 runs redundantly), so the late h polls go away
-    constexpr bool XL = HL && WRNN_RR_X_LOCAL;
+    constexpr bool XL = true;
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * RX_GROUP);
 
     // ---- weights -------------------------------------------------------------------------

@@ -48,13 +48,15 @@ constexpr int WL_RI = WL_X1 + 256;               // RowInfo of the group's rows 
 constexpr int WL_FAIL = WL_RI + 16 * 6;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
+constexpr int WL_P1F = WL_BIAS + 112;            // P1-ready step tags of waves 4-7 (ints)
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
 constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
 constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
+constexpr int WL_P1 = WL_PH;                     // P1(t + 1) per cell [256] float4 (overlays WL_PH)
 constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(WL_BIAS + 112 <= WL_PS, "small LDS arrays overflow their 8 KiB");
+static_assert(WL_P1F + 4 <= WL_PS, "small LDS arrays overflow their 8 KiB");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -87,10 +89,7 @@ __device__ __forceinline__ bool w_poll8(rsrc_t xr, unsigned voff, unsigned so, u
     unsigned nsp = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) cc[i] = (u4v){0u, want, 0u, want};
-#ifndef WRNN_WIDE_POLL_ALL_FIRST
-#define WRNN_WIDE_POLL_ALL_FIRST 1
-#endif
-    if (WRNN_WIDE_POLL_ALL_FIRST) {
+    {
         // first pass: all 8 couples in flight at once -- the data is often there already
         // (one L2 round trip instead of two); then spin on couple 0 as below
         bool ok = true;
@@ -192,9 +191,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     }
     if (tid < R) reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
     if (tid == 0) lds[WL_FAIL] = 0.f;
-#ifndef WRNN_WIDE_BIAS_LDS
-#define WRNN_WIDE_BIAS_LDS 1
-#endif
     // biases of the slot in LDS: read per step by the epilogues (a global load there would
     // hold up the wave's next poll behind its latency)
     if (tid < 112) {
@@ -217,9 +213,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     // per-step operands of the cell, loaded right after the hop E poll:
     //   pc[0..2] GRU2 cond (W_ih2[:, 512:] a2 + b_ih2), pc[3] fc1 cond, pc[4] fc2 cond (frame t)
     //   pg       Gumbel noise of (row, class cu) at step t
-    //   pp       P1(t + 1) of (row, unit cu): r, z, n of W_ih1 I(c) + b_ih1, then cI
+    // (P1(t + 1), GRU1's input term, is formed from the per-frame tables in the hop D window,
+    // p1_loads / p1_form below)
     float pc[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, pg = 0.f;
-    float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
     auto prefetch = [&](int t) {
         if (!cell) return;
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[cn];
@@ -232,11 +228,53 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         pc[3] = bld(fcr, fo + (unsigned)(a.oF1 + uu) * 4u, 0);
         pc[4] = bld(fcr, fo + (unsigned)(a.oF2 + uu) * 4u, 0);
         pg = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + crow) * a.n_classes), (unsigned)uu * 4u, 0);
-        const int tn = t + 1 < a.S ? t + 1 : a.S - 1;
-        pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            mk_rsrc(a.P1 + ((size_t)tn * a.B + crow) * 4 * kPH),
-                                            (unsigned)uu * 16u, 0, 0));
     };
+    // P1(tau) of cell (row n, unit u): (r, z, n) of W_ih1 (I c) + b_ih1, then I c + b_I. With
+    // the per-frame tables (a.p1q, runtime.hip pack_p1) it is formed here as k_persist's ring
+    // producers form it (kernels_persist.hip p1_loads / p1_store: k_p1_expand's fma chain
+    // without its zero tap): the phase's 4 taps, 4 frame rows of Q and one of Aq, from
+    // L2-resident tables (a row stays in one frame for 200 steps) -- no [S][B][4H] stream.
+    // Waves 4-7 (no epilogue cells, idle while waves 0-3 run the fc3 epilogue, hop D and GRU1)
+    // form P1(t + 1) of cell i = tid - 256 and hand it over through LDS (WL_P1) with a per-wave
+    // step tag (WL_P1F): wave 4 + v serves exactly the cells of wave v.
+    auto p1_make = [&](int n, int u, int tau) -> float4 {
+        tau = tau < a.S ? tau : a.S - 1;
+        int uu = u;
+        asm volatile("" : "+v"(uu));
+        if (a.p1q == nullptr)  // the [S][B][4H] stream (WRNN_P1_RING=0)
+            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  mk_rsrc(a.P1 + ((size_t)tau * a.B + g0 + kPG * n) * 4 * kPH),
+                                                  (unsigned)uu * 16u, 0, 0));
+        const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
+        const unsigned p = (unsigned)(ri.rel0 + tau);
+        const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
+        const unsigned f = p / (unsigned)a.hop, sph = in ? p - f * (unsigned)a.hop : 0u;
+        const unsigned s0 = in ? (unsigned)ri.fbase - 1u + f + (sph >= (unsigned)a.p1split ? 1u : 0u)
+                               : (unsigned)ri.fbase;
+        constexpr unsigned kRow = 4u * kPH * 4u;  // bytes per frame slot
+        const unsigned col = (unsigned)uu * 16u;
+        const float4 tk = __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(mk_rsrc(a.p1taps), sph * 16u, 0, 0));
+        const rsrc_t qr = mk_rsrc(a.p1q);
+        float4 tq[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            tq[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   qr, (in ? s0 + (unsigned)k : s0) * kRow + col, 0, 0));
+        const float4 ta = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         mk_rsrc(a.p1a), (in ? (unsigned)ri.fbase + 1u + f : s0) * kRow + col, 0, 0));
+        float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float kk[4] = {tk.x, tk.y, tk.z, tk.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            m.x = fmaf(kk[k], tq[k].x, m.x);
+            m.y = fmaf(kk[k], tq[k].y, m.y);
+            m.z = fmaf(kk[k], tq[k].z, m.z);
+            m.w = fmaf(kk[k], tq[k].w, m.w);
+        }
+        return make_float4(p_add(m.x, ta.x), p_add(m.y, ta.y), p_add(m.z, ta.z), p_add(m.w, ta.w));
+    };
+    if (tid < 4) reinterpret_cast<int*>(lds + WL_P1F)[tid] = 0;
     __syncthreads();
     // initial hop E: x1, h1 of step t0 (k_persist_init) with tag t0 + 1
     pub(WB_X1, cell ? lds[WL_X1 + cn * 16 + cul] : 0.f, (unsigned)a.t0 + 1u);
@@ -343,8 +381,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
                     lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + j * 16 + ul]
-                                                    : bld(mk_rsrc(a.b_hh1), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                        p_add(s, lds[WL_BIAS + j * 16 + ul]);
                 }
         }
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
@@ -406,8 +443,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + rn) * 16 + ul];
                     lds[WL_GH2 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, WRNN_WIDE_BIAS_LDS ? lds[WL_BIAS + 48 + j * 16 + ul]
-                                                    : bld(mk_rsrc(a.b_hh2), (unsigned)(16 * w + ul) * 4u, (unsigned)(j * kPH) * 4u));
+                        p_add(s, lds[WL_BIAS + 48 + j * 16 + ul]);
                 }
         }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
@@ -495,8 +531,23 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // ============= GRU1 of step t + 1 for the slot's units -> publish x1, h1 ========
             //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
             // (at the last step it runs on clamped inputs and nobody reads the result)
+            // P1(t + 1) of this wave's cells from wave 4 + v (formed in this window)
+            {
+                const volatile int* tag = reinterpret_cast<const volatile int*>(lds + WL_P1F) + v;
+                const unsigned t0s = p_now();
+                while (*tag != (int)seq) {
+                    if (p_now() - t0s > kSpinTicks) {
+                        if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
+                        fail = true;
+                        break;
+                    }
+                }
+                asm volatile("" ::: "memory");
+            }
+            if (fail) lds[WL_FAIL] = 1.f;
             float x1 = 0.f;
             if (cell) {
+                const float4 pp = reinterpret_cast<const float4*>(lds + WL_P1)[tid];
                 const float* gh = lds + WL_GH1 + cn * 16 + cul;
                 h1r = p_gru(fmaf(vj0, x, pp.x), fmaf(vj1, x, pp.y), fmaf(vj2, x, pp.z), gh[0], gh[256],
                             gh[512], h1r);
@@ -505,6 +556,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             }
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
+        } else {
+            // waves 4-7: P1(t + 1) of cell i = tid - 256 (the cell of thread i of waves 0-3)
+            // into WL_P1, then the wave's tag. WL_P1 overlays the W_hh1 h1 partials, which
+            // are dead until the next step's hop A: GRU1 reads it before this workgroup's
+            // x1 publish, i.e. before any wave passes the next step's stage-A barrier.
+            const int i = tid - 256;
+            if (i < 16 * R) reinterpret_cast<float4*>(lds + WL_P1)[i] = p1_make(i >> 4, 16 * w + (i & 15), t + 1);
+            asm volatile("" ::: "memory");  // the tag after the wave's P1 store (LDS in order)
+            if (l == 0) reinterpret_cast<volatile int*>(lds + WL_P1F)[v - 4] = (int)seq;
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);

@@ -201,10 +201,9 @@ __device__ __forceinline__ void half_argmax(float& v, int& k) {
 // Buffer-resource access: a uniform (SGPR) base and a 32-bit per-lane byte offset, so no
 // 64-bit per-lane addresses stay live across the step loop.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
-#ifndef WRNN_POLL_CPOL
-#define WRNN_POLL_CPOL 2
-#endif
-constexpr int kCpNT = WRNN_POLL_CPOL;  // cache policy: non-temporal (served by L2, bypasses the CU's L1)
+// cache policy of the polls: non-temporal (served by L2, bypasses the CU's L1); sc1 measured
+// the same (6.661 vs 6.677 us per C2 step)
+constexpr int kCpNT = 2;
 __device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
@@ -228,7 +227,7 @@ __device__ __forceinline__ void bst_tag(float v, unsigned tag, rsrc_t r, unsigne
 // Poll M 16-byte couples (two tagged pairs each) until every tag equals `want`, storing the
 // values to LDS (dst[m], float2) on every pass; the last pass, the one that saw all tags, wins.
 // False on an abort / timeout (error code set).
-template <int M>
+template <int M, bool ALL_FIRST = false>
 __device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M], unsigned so,
                                              unsigned want, float2* const (&dst)[M], unsigned* ctl) {
     // spin on the first couple only (a thread's couples all come from one producer slot), then
@@ -237,13 +236,10 @@ __device__ __forceinline__ bool poll_couples(rsrc_t xr, const unsigned (&off)[M]
     // value is seen about half an L2 round trip sooner than with one poll at a time.
     const unsigned t0 = p_now();
     unsigned n = 0;
-#ifndef WRNN_POLL_ALL_FIRST
-#define WRNN_POLL_ALL_FIRST 0
-#endif
-    if (WRNN_POLL_ALL_FIRST) {
+    if constexpr (ALL_FIRST) {
         // first pass: every couple in flight at once -- when the data is there already this is
         // one L2 round trip instead of two (measured per kernel: geneing 3.73 -> 3.57 us/step;
-        // fatchord 6.53 -> 6.72 and runtimeracer 8.67 -> 8.83 slower, so off there)
+        // fatchord 6.53 -> 6.72 and runtimeracer 8.67 -> 8.83 slower, so geneing only)
         bool ok = true;
         u4v c[M];
 #pragma unroll

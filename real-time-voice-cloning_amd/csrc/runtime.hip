@@ -1762,7 +1762,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     a.oF2 = W.oF2;
     a.P1 = P.P1.f();
     a.cI = ws.cI.f();
-    if (h->p1_ring && !rr && !gen) {  // k_persist forms P1 in-kernel (wide launches ignore these)
+    if (h->p1_ring && !rr && !gen) {  // k_persist and k_persist_wide form P1 in-kernel
         a.p1q = ws.q4.f();
         a.p1a = ws.a4.f();
         a.p1taps = W.p1taps + (size_t)h->hop * 8;  // the [hop][4] table
@@ -2212,10 +2212,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     }
     const int Bp = use_p ? Bplan : B;  // persistent groups carry nr rows per launch
     h->p_plan = use_p ? lplan : std::vector<wrnn_handle::PLaunch>();
-    // P1: the register-resident fatchord launches form it in-kernel (ring) when the per-frame
-    // form exists; the [S][B][4H] stream is written only for the other kernels
-    bool any_wide = false;
-    for (const auto& L : h->p_plan) any_wide |= L.wide;
+    // P1: the fatchord launches (register-resident and wide) form it in-kernel when the
+    // per-frame form exists; the [S][B][4H] stream is written only for the other kernels
     // per call: the ring unless a k_persist launch of the plan spills more with it than with
     // the stream (measured: MOL at 3 rows per group spills one register with the ring and
     // runs 6.87 against 6.53 us per step)
@@ -2225,7 +2223,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
                 persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
             h->p1_ring = false;
-    h->p1_stream = use_p && (!h->p1_ring || any_wide);
+    h->p1_stream = use_p && !h->p1_ring;  // (the wide launches form P1 in-kernel too)
     CHECK(ensure_workspace(h, Bp, S, P, Fr + 1, Tmax));
     auto& ws = h->ws;
     h->last_B = B;
