@@ -90,8 +90,9 @@ typedef struct wrnn_handle wrnn_handle;
  * progress_callback arguments (fatchord_version.py:234-236): step index i, seq_len, b_size,
  * gen_rate in kHz -- as soon as every fold row has finished step i (PERSIST: the kernels
  * publish their step count to host-mapped memory; CHAIN: between 100-step graphs). Return
- * non-zero to abort (WRNN_ERR_ABORTED): no further callbacks; PERSIST stops at the end of the
- * running launch. */
+ * non-zero to abort (WRNN_ERR_ABORTED): no further callbacks; PERSIST sets a host-mapped abort
+ * word that every XCD group checks at its next progress point, so the launches drain within
+ * ~100 steps (the reference stops at the raising step). */
 typedef int (*wrnn_progress_fn)(void* user, int i, int seq_len, int b_size, double gen_rate_khz);
 
 /* Library / device info. */

@@ -80,7 +80,8 @@ static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 Ki
 
 
 // P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
-template <int NR, bool FC3R, bool MOL, bool P1R>
+// DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
+template <int NR, bool FC3R, bool MOL, bool P1R, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -613,7 +614,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, lds[L_BCLS + og]);
-                    p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
                     if (!MOL)
                         val = p_add(l, pgum);
                     else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
@@ -926,24 +927,14 @@ size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
-    static bool attr = false;
-    const size_t lds = persist_lds_bytes();
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist<NR, FC3R, MOL, P1R>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    static int coresident = 0;
-    if (hipError_t e = persist_coresident((const void*)k_persist<NR, FC3R, MOL, P1R>, lds, &coresident); e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_persist<NR, FC3R, MOL, P1R>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
-    return hipGetLastError();
+    if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, true>>(persist_lds_bytes(), a, s);
+    return persist_launch<k_persist<NR, FC3R, MOL, P1R, false>>(persist_lds_bytes(), a, s);
 }
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 int persist_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 

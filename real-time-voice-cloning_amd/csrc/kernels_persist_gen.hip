@@ -80,7 +80,8 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
 }  // namespace
 
 // MODE: 0 RAW (categorical, 'BITS'), 1 MOL, 2 BETA (geneing 'RAW'); each its own instantiation
-template <int NR, int MODE>
+// DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
+template <int NR, int MODE, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, bcls);
-                    p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
                     // (MOL / BETA: the logit itself, published after the gh1 poll below)
                     val = MODE == 0 ? p_add(l, pgum) : l;
                 }
@@ -476,24 +477,14 @@ size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
 // raise the register allocation of the RAW / MOL variants
 template <int NR, int MODE>
 hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
-    static bool attr = false;
-    const size_t lds = persist_gen_lds_bytes();
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist_gen<NR, MODE>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    static int coresident = 0;
-    if (hipError_t e = persist_coresident((const void*)k_persist_gen<NR, MODE>, lds, &coresident); e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_persist_gen<NR, MODE>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
-    return hipGetLastError();
+    if (a.dbg.out) return persist_launch<k_persist_gen<NR, MODE, true>>(persist_gen_lds_bytes(), a, s);
+    return persist_launch<k_persist_gen<NR, MODE, false>>(persist_gen_lds_bytes(), a, s);
 }
 
 template <int NR, int MODE>
 int persist_gen_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, MODE>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, MODE, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 

@@ -178,7 +178,8 @@ __device__ __forceinline__ bool poll_hop_hx(rsrc_t xr, unsigned so, unsigned seq
 
 }  // namespace
 
-template <int NR, bool MOL>
+// DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
+template <int NR, bool MOL, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 float val = -INFINITY;
                 if (has_cls) {
                     const float l = p_add(s0, bcls);
-                    p_dbg_logit(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
                     // (MOL: the logit itself, published after the barrier below)
                     val = MOL ? l : p_add(l, pgum);
                 }
@@ -781,24 +782,14 @@ size_t persist_rr_xbuf_floats() { return (size_t)kPG * RX_GROUP; }
 
 template <int NR, bool MOL>
 hipError_t launch_persist_rr_t(const PersistRRArgs& a, hipStream_t s) {
-    static bool attr = false;
-    const size_t lds = persist_rr_lds_bytes();
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_persist_rr<NR, MOL>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    static int coresident = 0;
-    if (hipError_t e = persist_coresident((const void*)k_persist_rr<NR, MOL>, lds, &coresident); e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_persist_rr<NR, MOL>), dim3(kPG * kPM), dim3(kPT), lds, s, a);
-    return hipGetLastError();
+    if (a.dbg.out) return persist_launch<k_persist_rr<NR, MOL, true>>(persist_rr_lds_bytes(), a, s);
+    return persist_launch<k_persist_rr<NR, MOL, false>>(persist_rr_lds_bytes(), a, s);
 }
 
 template <int NR, bool MOL>
 int persist_rr_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 

@@ -123,6 +123,23 @@ inline hipError_t persist_coresident(const void* fn, size_t lds, int* cached) {
     return *cached == 1 ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
 }
 
+// Host side: launch one persistent kernel instance K (kPG * kPM workgroups of kPT threads,
+// `lds` bytes of dynamic LDS): its LDS attribute once, the co-residency check, the launch.
+template <auto K, typename Args>
+inline hipError_t persist_launch(size_t lds, const Args& a, hipStream_t s) {
+    const void* fn = reinterpret_cast<const void*>(K);
+    static bool attr = false;
+    if (!attr) {
+        if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); e != hipSuccess)
+            return e;
+        attr = true;
+    }
+    static int coresident = 0;
+    if (hipError_t e = persist_coresident(fn, lds, &coresident); e != hipSuccess) return e;
+    hipLaunchKernelGGL(K, dim3(kPG * kPM), dim3(kPT), lds, s, a);
+    return hipGetLastError();
+}
+
 // Progress of a launch for the host's progress callback (fatchord_version.py:234-236 calls
 // back at i % 100 == 0): after step t with t % 100 == 0, one lane publishes base + t + 1
 // steps done to a host-mapped word (vector store, system scope); the host polls it while the
@@ -147,8 +164,12 @@ __device__ __forceinline__ bool p_abort(unsigned* ctl, const unsigned* prog, int
 
 // Teacher-forced logit gate (debug only): the logit l of (row, cls) at a step the host asked
 // for goes to dbg.out[slot][row][cls] (wrnn_debug_logits); nothing when the capture is off.
+// Only the DBG instances of the kernels record (launched when the capture is on), so the
+// production instances carry no trace of it (registers are at the limit there).
+template <bool DBG>
 __device__ __forceinline__ void p_dbg_logit(const DbgLogits& d, int t, int row, int cls, int B,
                                             int n, float l) {
+    if constexpr (!DBG) return;
     if (d.out == nullptr) return;
     const int k = __builtin_amdgcn_readfirstlane(d.map[t]);
     if (k >= 0) d.out[((size_t)k * B + row) * n + cls] = l;

@@ -162,7 +162,8 @@ struct wrnn_handle {
 
     // ---- workspace (capacity keyed on rows/steps)
     struct Workspace {
-        int B = 0, S = 0, Pcap = 0, Fcap = 0, Tcap = 0;
+        int B = 0, S = 0, Pcap = 0, Fcap = 0, Tcap = 0, Ncap = 0;
+        int N = 0;  // frame columns of the MelResNet activations of the last call (sum of T)
         DevBuf slots[SL_COUNT];
         DevBuf labels, samples, noise, cI, fcond, rows, stamps;
         DevBuf mel_in, act0, act1, Rb, up1, up2, melup;
@@ -1061,14 +1062,16 @@ int pick_rt(int B, int* nrt) {
     return best;
 }
 
-int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tmax) {
+int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tmax, int Tsum) {
     auto& ws = h->ws;
-    const bool grow = B > ws.B || S > ws.S || Pneed > ws.Pcap || Fneed > ws.Fcap || Tmax > ws.Tcap;
+    const bool grow = B > ws.B || S > ws.S || Pneed > ws.Pcap || Fneed > ws.Fcap || Tmax > ws.Tcap ||
+                      Tsum > ws.Ncap;
     if (!grow) return WRNN_OK;
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     h->graphs.clear();
     const int nB = std::max(B, ws.B), nS = std::max(S, ws.S);
     const int nP = std::max(Pneed, ws.Pcap), nF = std::max(Fneed, ws.Fcap), nT = std::max(Tmax, ws.Tcap);
+    const int nN = std::max(Tsum, ws.Ncap);
     for (int s = 0; s < SL_CI; ++s) {
         const int w = h->slot_width(s);
         if (w == 0) continue;
@@ -1086,7 +1089,8 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
     CHECK(ws.cI.alloc((size_t)nS * nB * h->H * sizeof(float)));  // folded [t][row][H]
     CHECK(ws.fcond.alloc((size_t)nF * h->cond_width * sizeof(float)));
     CHECK(ws.rows.alloc((size_t)nB * sizeof(RowInfo)));
-    // upsample scratch for one utterance of <= nT frames
+    // MelResNet activations of every utterance of a call side by side (nN frame columns);
+    // mel upsample scratch for one utterance of <= nT frames
     const int tot = h->hop;  // product of factors
     ws.act0.release();
     ws.act1.release();
@@ -1094,9 +1098,9 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
     ws.up1.release();
     ws.up2.release();
     ws.melup.release();
-    CHECK(ws.act0.alloc((size_t)h->C * nT * sizeof(float)));
-    CHECK(ws.act1.alloc((size_t)h->C * nT * sizeof(float)));
-    CHECK(ws.Rb.alloc((size_t)h->R * nT * sizeof(float)));
+    CHECK(ws.act0.alloc((size_t)h->C * nN * sizeof(float)));
+    CHECK(ws.act1.alloc((size_t)h->C * nN * sizeof(float)));
+    CHECK(ws.Rb.alloc((size_t)h->R * nN * sizeof(float)));
     size_t w1 = (size_t)(nT + 2 * h->cfg.pad) * h->cfg.upsample_factors[0];
     size_t w2 = w1 * (h->cfg.n_upsample > 1 ? h->cfg.upsample_factors[1] : 1);
     CHECK(ws.up1.alloc((size_t)h->feat * w1 * sizeof(float)));
@@ -1107,6 +1111,7 @@ int ensure_workspace(wrnn_handle* h, int B, int S, int Pneed, int Fneed, int Tma
     ws.Pcap = nP;
     ws.Fcap = nF;
     ws.Tcap = nT;
+    ws.Ncap = nN;
     return WRNN_OK;
 }
 
@@ -1129,36 +1134,40 @@ static bool p1_ring_ok(const wrnn_handle* h) {
            p1_frames_enabled();
 }
 
-// ---- upsample network + conditioning for one utterance --------------------------------
-int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
-                 int row0, int fbase, float* P1out) {
+// ---- MelResNet of every utterance of a call as one batch of frame columns ---------------
+// fatchord_version.py:27-44 (runtimeracer / geneing the same): conv_in (k = 2 pad + 1, no
+// padding) per utterance -- its im2col reads that utterance's zero-padded mel -- into its own
+// columns [col0, col0 + T) of act0, then the 2 x res_blocks 1x1 convs (BatchNorm folded, ReLU /
+// residual) and conv_out over all N = sum(T) columns at once: one launch per layer for the
+// whole call instead of one per layer and utterance.
+int run_resnet(wrnn_handle* h, int n_utts, const float* const* mels, const int* T, const int* col0, int N) {
     auto& ws = h->ws;
     hipStream_t st = h->stream;
-    const int C = h->C, R = h->R, H = h->H;
+    const int C = h->C, R = h->R;
     const int ksz = 2 * h->cfg.pad + 1;
-    const int L = T * h->hop;
-    // MelResNet: conv_in (k = 2*pad+1, no padding) on the mel padded by `pad` frames
-    GemmA a{};
-    GemmB b{};
-    GemmEp e{};
-    a.kind = 0;
-    a.p = h->Wci;
-    a.ld = h->feat * ksz;
-    b.kind = 1;
-    b.p = d_mel;
-    b.T = T;
-    b.pad = 0;  // im2col index n + kk over the padded mel: padded(i) = mel(i - pad)
-    b.ksz = ksz;
-    // out frame n uses padded[n + kk] = mel[n + kk - pad]
-    b.pad = h->cfg.pad;
-    e.kind = 2;
-    e.D = ws.act0.f();
-    e.ld = T;
-    e.alpha = h->bn_a;
-    e.beta = h->bn_b;
-    e.relu = 1;
-    e.res = nullptr;
-    HIPC(launch_gemm(C, T, h->feat * ksz, a, b, e, st));
+    if (N > ws.Ncap) return fail(WRNN_ERR_INVALID, "MelResNet columns exceed the workspace");
+    ws.N = N;
+    for (int u = 0; u < n_utts; ++u) {
+        GemmA a{};
+        GemmB b{};
+        GemmEp e{};
+        a.kind = 0;
+        a.p = h->Wci;
+        a.ld = h->feat * ksz;
+        b.kind = 1;  // im2col: out frame n uses padded[n + kk] = mel[n + kk - pad]
+        b.p = mels[u];
+        b.T = T[u];
+        b.pad = h->cfg.pad;
+        b.ksz = ksz;
+        e.kind = 2;
+        e.D = ws.act0.f() + col0[u];
+        e.ld = N;
+        e.alpha = h->bn_a;
+        e.beta = h->bn_b;
+        e.relu = 1;
+        e.res = nullptr;
+        HIPC(launch_gemm(C, T[u], h->feat * ksz, a, b, e, st));
+    }
     for (int i = 0; i < h->cfg.res_blocks; ++i) {
         GemmA a1{};
         GemmB b1{};
@@ -1168,14 +1177,14 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         a1.ld = C;
         b1.kind = 0;
         b1.p = ws.act0.f();
-        b1.ld = T;
+        b1.ld = N;
         e1.kind = 2;
         e1.D = ws.act1.f();
-        e1.ld = T;
+        e1.ld = N;
         e1.alpha = h->bn_a + (size_t)(1 + 2 * i) * C;
         e1.beta = h->bn_b + (size_t)(1 + 2 * i) * C;
         e1.relu = 1;
-        HIPC(launch_gemm(C, T, C, a1, b1, e1, st));
+        HIPC(launch_gemm(C, N, C, a1, b1, e1, st));
         GemmA a2{};
         GemmB b2{};
         GemmEp e2{};
@@ -1184,32 +1193,41 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         a2.ld = C;
         b2.kind = 0;
         b2.p = ws.act1.f();
-        b2.ld = T;
+        b2.ld = N;
         e2.kind = 2;
         e2.D = ws.act0.f();
-        e2.ld = T;
+        e2.ld = N;
         e2.alpha = h->bn_a + (size_t)(2 + 2 * i) * C;
         e2.beta = h->bn_b + (size_t)(2 + 2 * i) * C;
         e2.relu = 0;
         e2.res = ws.act0.f();
-        HIPC(launch_gemm(C, T, C, a2, b2, e2, st));
+        HIPC(launch_gemm(C, N, C, a2, b2, e2, st));
     }
-    {
-        GemmA a3{};
-        GemmB b3{};
-        GemmEp e3{};
-        a3.kind = 0;
-        a3.p = h->Wco;
-        a3.ld = C;
-        b3.kind = 0;
-        b3.p = ws.act0.f();
-        b3.ld = T;
-        e3.kind = 1;
-        e3.D = ws.Rb.f();
-        e3.ld = T;
-        e3.bias = h->bco;
-        HIPC(launch_gemm(R, T, C, a3, b3, e3, st));
-    }
+    GemmA a3{};
+    GemmB b3{};
+    GemmEp e3{};
+    a3.kind = 0;
+    a3.p = h->Wco;
+    a3.ld = C;
+    b3.kind = 0;
+    b3.p = ws.act0.f();
+    b3.ld = N;
+    e3.kind = 1;
+    e3.D = ws.Rb.f();
+    e3.ld = N;
+    e3.bias = h->bco;
+    HIPC(launch_gemm(R, N, C, a3, b3, e3, st));
+    return WRNN_OK;
+}
+
+// ---- upsample + conditioning for one utterance (its MelResNet output: Rb columns col0..) --
+int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
+                 int row0, int fbase, float* P1out, int col0) {
+    auto& ws = h->ws;
+    hipStream_t st = h->stream;
+    const int H = h->H;
+    const int L = T * h->hop;
+    const float* Rb = ws.Rb.f() + col0;  // aux channel c of frame f: Rb[c * ws.N + f]
     // PERSIST with the per-frame P1 (pack_p1): no upsampled mel is needed at all
     const bool p1f = P1out && h->pw.p1x4 && h->pw.p1taps_ok && p1_frames_enabled();
     h->melup_valid = !p1f;
@@ -1247,8 +1265,8 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         a4.n_mel = h->feat;
         a4.L = L;
         a4.hop = h->hop;
-        a4.R = ws.Rb.f();
-        a4.ldr = T;
+        a4.R = Rb;
+        a4.ldr = ws.N;
         a4.r_off = 0;
         a4.n_aux = h->A - 1;
         a4.Bu = Bu;
@@ -1284,7 +1302,8 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
             eq.ld = np;
             eq.bias = h->pw.zero_np;
             HIPC(launch_gemm(T + 1, np, h->feat, aq, bq, eq, st));
-            aq.R = ws.Rb.f();  // aux channels 0 .. A-2 (the I slice, as a4.r_off / n_aux)
+            aq.R = Rb;  // aux channels 0 .. A-2 (the I slice, as a4.r_off / n_aux)
+            aq.ldr = ws.N;
             bq.p = h->pw.M1T + (size_t)h->feat * np;
             eq.D = ws.a4.f() + (size_t)fbase * np;
             eq.bias = h->pw.bP1;
@@ -1310,8 +1329,8 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         GemmB b5{};
         GemmEp e5{};
         a5.kind = 2;
-        a5.R = ws.Rb.f();
-        a5.ldr = T;
+        a5.R = Rb;
+        a5.ldr = ws.N;
         a5.r_off = ac.slice * h->A;
         b5.kind = 0;
         b5.p = ac.WT;
@@ -2224,7 +2243,15 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
             h->p1_ring = false;
     h->p1_stream = use_p && !h->p1_ring;  // (the wide launches form P1 in-kernel too)
-    CHECK(ensure_workspace(h, Bp, S, P, Fr + 1, Tmax));
+    // MelResNet frame columns: utterance u at [col0[u], col0[u] + T[u])
+    std::vector<int> Ts(n_utts), col0(n_utts);
+    int Tsum = 0;
+    for (int u = 0; u < n_utts; ++u) {
+        Ts[u] = plan[u].T;
+        col0[u] = Tsum;
+        Tsum += plan[u].T;
+    }
+    CHECK(ensure_workspace(h, Bp, S, P, Fr + 1, Tmax, Tsum));
     auto& ws = h->ws;
     h->last_B = B;
     h->last_Bp = Bp;
@@ -2274,9 +2301,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         CHECK(ws.a4.alloc(bytes));
         HIPC(hipMemsetAsync(ws.q4.p, 0, bytes, h->stream));
     }
+    CHECK(run_resnet(h, n_utts, mels, Ts.data(), col0.data(), Tsum));
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
-                           plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr));
+                           plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr, col0[u]));
     int rc = WRNN_OK;
     if (use_p) {
         rc = run_persist(h, S, cb, user);
@@ -2299,7 +2327,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             if (h->pw.p1x4)  // cI was not written (P1 carried it): conditioning again, cI only
                 for (int u = 0; u < n_utts; ++u)
                     CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0,
-                                       S, Bp, plan[u].row0, plan[u].fbase, nullptr));
+                                       S, Bp, plan[u].row0, plan[u].fbase, nullptr, col0[u]));
             h->last_B = Bp;  // chain runs every padded row (cI stride is Bp)
             rc = run_chain(h, S, cb, user);
             h->last_B = B;
@@ -2730,7 +2758,9 @@ int wrnn_debug_upsample(wrnn_handle* h, float* mel_out, size_t mel_cap, float* a
     }
     if (aux_out) {
         if (aux_cap < na) return fail(WRNN_ERR_CAPACITY, "aux capacity");
-        HIPC(hipMemcpy(aux_out, h->ws.Rb.p, na * sizeof(float), hipMemcpyDeviceToHost));
+        // utterance 0's columns [0, T0) of the call's [R][N] MelResNet output
+        HIPC(hipMemcpy2D(aux_out, (size_t)h->last_T0 * sizeof(float), h->ws.Rb.p, (size_t)h->ws.N * sizeof(float),
+                         (size_t)h->last_T0 * sizeof(float), h->R, hipMemcpyDeviceToHost));
     }
     return WRNN_OK;
 }
