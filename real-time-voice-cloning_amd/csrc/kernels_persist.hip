@@ -847,14 +847,7 @@ hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// RAW Gumbel noise g = -log(q), q the contract's Exp(1) variate (philox.h exp1_from_u32, its
-// float64 log kept exact): argmax_k (l_k + g_k) is the decision of argmax_k ((softmax(l)_k / sum)
-// / q_k). The second log runs in fp32 (logf, ~1 ulp: the order of the fp32 rounding the
-// reference's own p / q carries; both logs in float64 took 0.88 instead of 0.54 ms per C2 call,
-// labels unchanged).
-__device__ __forceinline__ float gumbel_of(uint32_t x) {
-    return -logf(exp1_from_u32(x));
-}
+// RAW Gumbel noise of every (step, row, class): philox.h gumbel_of
 __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int ng,
                                                 const RowInfo* rows, uint32_t k0, uint32_t k1) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r, k4)

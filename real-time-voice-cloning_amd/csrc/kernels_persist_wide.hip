@@ -27,6 +27,7 @@
 // its next barrier.
 #include "wrnn_kernels.h"
 #include "persist_common.h"
+#include "philox.h"
 
 namespace wrnn {
 
@@ -37,6 +38,12 @@ constexpr int WV = 8 * 8 * 4 * 16 * 4;  // one vector buffer: [e 8][i 8][c 4][n 
 enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
 constexpr int WX_D = WB_N * WV;                    // candidates [n 16][slot 32] (value, tag|class)
 constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
+// Per-group operand ring (PersistArgs::wring, runtime.hip persist_wide_ring_floats): P1 (r, z, n of
+// W_ih1 (I c) + b_ih1, then I c + b_I) and the Gumbel noise of every cell for 4 steps,
+// [slot = step & 3][row n][unit / class], formed in-kernel three steps ahead (see the fc3 window)
+constexpr int WR_SLOTS = 4;
+constexpr int WR_G = WR_SLOTS * 16 * kPH * 4;  // P1: float4 [4][16][512] at 0; noise: float [4][16][512]
+constexpr int WR_GROUP = WR_G + WR_SLOTS * 16 * kPH;
 
 // ---- LDS (floats) -------------------------------------------------------------------------
 // Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
@@ -48,15 +55,13 @@ constexpr int WL_RI = WL_X1 + 256;               // RowInfo of the group's rows 
 constexpr int WL_FAIL = WL_RI + 16 * 6;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
-constexpr int WL_P1F = WL_BIAS + 112;            // P1-ready step tags of waves 4-7 (ints)
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
 constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
 constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
-constexpr int WL_P1 = WL_PH;                     // P1(t + 1) per cell [256] float4 (overlays WL_PH)
 constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(WL_P1F + 4 <= WL_PS, "small LDS arrays overflow their 8 KiB");
+static_assert(WL_BIAS + 112 <= WL_PS, "small LDS arrays overflow their 8 KiB");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -178,8 +183,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #define WR(T, ks) f4c(wq[4 * (T) + (ks) / 4], (ks) % 4)
     const float4* hh2 = reinterpret_cast<const float4*>(lds + WL_HH2);
     // ---- state and per-cell constants --------------------------------------------------
-    float h1r = 0.f, h2r = 0.f;
+    float h1r = 0.f, h2r = 0.f, vj0 = 0.f, vj1 = 0.f, vj2 = 0.f, w0u = 0.f;
     if (cell) {
+        vj0 = a.v[cu];
+        vj1 = a.v[kPH + cu];
+        vj2 = a.v[2 * kPH + cu];
+        w0u = a.w0[cu];
         h1r = a.st_h1[(size_t)crow * kPH + cu];
         h2r = a.st_h2[(size_t)crow * kPH + cu];
         lds[WL_X1 + cn * 16 + cul] = a.st_x1[(size_t)crow * kPH + cu];
@@ -208,15 +217,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                                                    xr, o_prod, (unsigned)(hb * WV) * 4u, 0);
     };
     const rsrc_t fcr = mk_rsrc(a.fcond);
-    // per-step operands of the cell, loaded right after the hop E poll:
+    const rsrc_t rr = mk_rsrc(a.wring + (size_t)g * WR_GROUP);  // this group's operand ring
+    // per-step operands of the cell, loaded right after the hop E poll (L2-resident: the
+    // per-frame tables and the ring):
     //   pc[0..2] GRU2 cond (W_ih2[:, 512:] a2 + b_ih2), pc[3] fc1 cond, pc[4] fc2 cond (frame t)
-    //   pg       Gumbel noise of (row, class cu) at step t
-    // (P1(t + 1), GRU1's input term, is formed from the per-frame tables in the hop D window,
-    // p1_loads / p1_form below)
+    //   pg       Gumbel noise of (row, class cu) at step t        (ring slot t & 3)
+    //   pp       P1(t + 1) of (row, unit cu), consumed by GRU1     (ring slot (t + 1) & 3)
     float pc[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, pg = 0.f;
-#ifndef WRNN_WIDE_P1X
-#define WRNN_WIDE_P1X 1
-#endif
     float4 pp = make_float4(0.f, 0.f, 0.f, 0.f);
     auto prefetch = [&](int t) {
         if (!cell) return;
@@ -229,74 +236,78 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         pc[2] = bld(fcr, fo + (unsigned)(a.oG2 + 2 * kPH + uu) * 4u, 0);
         pc[3] = bld(fcr, fo + (unsigned)(a.oF1 + uu) * 4u, 0);
         pc[4] = bld(fcr, fo + (unsigned)(a.oF2 + uu) * 4u, 0);
-        pg = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + crow) * a.n_classes), (unsigned)uu * 4u, 0);
-#if WRNN_WIDE_P1X == 0  // A/B (temporary): P1 from the stream, loaded with the step's operands
-        {
-            const int tn = t + 1 < a.S ? t + 1 : a.S - 1;
-            pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                mk_rsrc(a.P1 + ((size_t)tn * a.B + crow) * 4 * kPH), (unsigned)uu * 16u, 0, 0));
-        }
-#endif
+        const unsigned cell_i = (unsigned)(cn * kPH + (uu & (kPH - 1)));
+        pg = bld(rr, (unsigned)WR_G * 4u + ((unsigned)(t & 3) * 16u * kPH + cell_i) * 4u, 0);
+        pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rr, ((unsigned)((t + 1) & 3) * 16u * kPH + cell_i) * 16u, 0, 0));
     };
-    // P1(tau) of cell (row n, unit u): (r, z, n) of W_ih1 (I c) + b_ih1, then I c + b_I. With
-    // the per-frame tables (a.p1q, runtime.hip pack_p1) it is formed here as k_persist's ring
-    // producers form it (kernels_persist.hip p1_loads / p1_store: k_p1_expand's fma chain
-    // without its zero tap): the phase's 4 taps, 4 frame rows of Q and one of Aq, from
-    // L2-resident tables (a row stays in one frame for 200 steps) -- no [S][B][4H] stream.
-    // Waves 4-7 (no epilogue cells, idle while waves 0-3 run the fc3 epilogue, hop D and GRU1)
-    // form P1(t + 1) of cell i = tid - 256 and hand it over through LDS (WL_P1) with a per-wave
-    // step tag (WL_P1F): wave 4 + v serves exactly the cells of wave v.
-    auto p1_make = [&](int n, int u, int tau) -> float4 {
-        tau = tau < a.S ? tau : a.S - 1;
+    // The ring entry of step tau for cell (row n, unit / class u), formed by waves 4-7 (no
+    // epilogue cells; idle while waves 0-3 run the fc3 epilogue, hop D and GRU1):
+    //  * P1(tau) as k_persist's ring producers form it (kernels_persist.hip p1_loads / p1_store:
+    //    k_p1_expand's fma chain without its zero tap) from the per-frame tables (a.p1q,
+    //    runtime.hip pack_p1): the phase's 4 taps, 4 frame rows of Q and one of Aq -- no
+    //    [S][B][4H] stream; with WRNN_P1_RING=0 (a.p1q null) copied from that stream instead;
+    //  * the Gumbel noise g = -log q of (tau, row, class u) with k_gumbel's operations
+    //    (philox.h gumbel_of) -- no [S][B][n] noise stream either.
+    auto ring_make = [&](int n, int u, int tau) {
+        const int tc = tau < a.S ? tau : a.S - 1;
         int uu = u;
         asm volatile("" : "+v"(uu));
-        if (a.p1q == nullptr)  // the [S][B][4H] stream (WRNN_P1_RING=0)
-            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  mk_rsrc(a.P1 + ((size_t)tau * a.B + g0 + kPG * n) * 4 * kPH),
-                                                  (unsigned)uu * 16u, 0, 0));
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
-        const unsigned p = (unsigned)(ri.rel0 + tau);
-        const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
-        const unsigned f = p / (unsigned)a.hop, sph = in ? p - f * (unsigned)a.hop : 0u;
-        const unsigned s0 = in ? (unsigned)ri.fbase - 1u + f + (sph >= (unsigned)a.p1split ? 1u : 0u)
-                               : (unsigned)ri.fbase;
-        constexpr unsigned kRow = 4u * kPH * 4u;  // bytes per frame slot
-        const unsigned col = (unsigned)uu * 16u;
-        const float4 tk = __builtin_bit_cast(
-            float4, __builtin_amdgcn_raw_buffer_load_b128(mk_rsrc(a.p1taps), sph * 16u, 0, 0));
-        const rsrc_t qr = mk_rsrc(a.p1q);
-        float4 tq[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            tq[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   qr, (in ? s0 + (unsigned)k : s0) * kRow + col, 0, 0));
-        const float4 ta = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         mk_rsrc(a.p1a), (in ? (unsigned)ri.fbase + 1u + f : s0) * kRow + col, 0, 0));
-        float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float kk[4] = {tk.x, tk.y, tk.z, tk.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            m.x = fmaf(kk[k], tq[k].x, m.x);
-            m.y = fmaf(kk[k], tq[k].y, m.y);
-            m.z = fmaf(kk[k], tq[k].z, m.z);
-            m.w = fmaf(kk[k], tq[k].w, m.w);
+        const unsigned cell_i = (unsigned)((tau & 3) * 16 * kPH + n * kPH + uu);
+        {
+            // the noise of class u (a padding class beyond n_classes is drawn and never used)
+            const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+            const uint32_t wd = (uu & 3) == 0 ? o.x : (uu & 3) == 1 ? o.y : (uu & 3) == 2 ? o.z : o.w;
+            bst(gumbel_of(wd), rr, (unsigned)WR_G * 4u + cell_i * 4u, 0);
         }
-        return make_float4(p_add(m.x, ta.x), p_add(m.y, ta.y), p_add(m.z, ta.z), p_add(m.w, ta.w));
+        __builtin_amdgcn_sched_barrier(0);  // (the noise's temporaries die before the P1 loads)
+        float4 v;
+        if (a.p1q == nullptr) {
+            v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               mk_rsrc(a.P1 + ((size_t)tc * a.B + g0 + kPG * n) * 4 * kPH),
+                                               (unsigned)uu * 16u, 0, 0));
+        } else {
+            const unsigned p = (unsigned)(ri.rel0 + tc);
+            const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
+            const unsigned f = p / (unsigned)a.hop, sph = in ? p - f * (unsigned)a.hop : 0u;
+            const unsigned s0 = in ? (unsigned)ri.fbase - 1u + f + (sph >= (unsigned)a.p1split ? 1u : 0u)
+                                   : (unsigned)ri.fbase;
+            constexpr unsigned kRow = 4u * kPH * 4u;  // bytes per frame slot
+            const unsigned col = (unsigned)uu * 16u;
+            const float4 tk = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(mk_rsrc(a.p1taps), sph * 16u, 0, 0));
+            const rsrc_t qr = mk_rsrc(a.p1q);
+            float4 tq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                tq[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       qr, (in ? s0 + (unsigned)k : s0) * kRow + col, 0, 0));
+            const float4 ta = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             mk_rsrc(a.p1a), (in ? (unsigned)ri.fbase + 1u + f : s0) * kRow + col, 0, 0));
+            float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float kk[4] = {tk.x, tk.y, tk.z, tk.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m.x = fmaf(kk[k], tq[k].x, m.x);
+                m.y = fmaf(kk[k], tq[k].y, m.y);
+                m.z = fmaf(kk[k], tq[k].z, m.z);
+                m.w = fmaf(kk[k], tq[k].w, m.w);
+            }
+            v = make_float4(p_add(m.x, ta.x), p_add(m.y, ta.y), p_add(m.z, ta.z), p_add(m.w, ta.w));
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rr, cell_i * 16u, 0, 0);
     };
     const bool lo = v < 4;  // waves 0-3 hold the epilogue cells
-    auto lo_w = [](int wv) { return wv < 4; };
-    if (tid < 4) reinterpret_cast<int*>(lds + WL_P1F)[tid] = 0;
-    __syncthreads();
-    // P1 hand-over, one step ahead: waves 4-7 form P1(t + 2) in the fc3 window of step t (tag
-    // t + 2); waves 0-3 take P1(t + 1) into registers at the end of stage A of step t, before
-    // the barrier after which that step's W_hh1 partials reuse the area, and GRU1 consumes it
-    // at the end of the step. Prologue: P1(t0 + 1).
-    if (!lo_w(v)) {
+    __syncthreads();  // RowInfo in LDS
+    // ring prologue: steps t0, t0 + 1, t0 + 2 (the loop forms t + 3 at step t). Drained before
+    // the barrier: the first reads come right after it.
+    if (!lo && tid - 256 < 16 * R) {
         const int i = tid - 256;
-        if (i < 16 * R) reinterpret_cast<float4*>(lds + WL_P1)[i] = p1_make(i >> 4, 16 * w + (i & 15), a.t0 + 1);
-        asm volatile("" ::: "memory");  // the tag after the wave's P1 store (LDS in order)
-        if (l == 0) reinterpret_cast<volatile int*>(lds + WL_P1F)[v - 4] = a.t0 + 1;
+        for (int k = 0; k < 3; ++k) ring_make(i >> 4, 16 * w + (i & 15), a.t0 + k);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __syncthreads();
     // initial hop E: x1, h1 of step t0 (k_persist_init) with tag t0 + 1
     pub(WB_X1, cell ? lds[WL_X1 + cn * 16 + cul] : 0.f, (unsigned)a.t0 + 1u);
     pub(WB_H1, h1r, (unsigned)a.t0 + 1u);
@@ -324,20 +335,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + 4 * (l >> 4)) = acc[j];
-        }
-        // P1(t + 1) of this wave's cells from wave 4 + v (formed a step ago)
-        if (WRNN_WIDE_P1X && v < 4) {
-            const volatile int* tag = reinterpret_cast<const volatile int*>(lds + WL_P1F) + v;
-            const unsigned t0s = p_now();
-            while (*tag != t + 1) {
-                if (p_now() - t0s > kSpinTicks) {
-                    if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
-                    fail = true;
-                    break;
-                }
-            }
-            asm volatile("" ::: "memory");
-            if (cell) pp = reinterpret_cast<const float4*>(lds + WL_P1)[tid];
         }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
@@ -516,18 +513,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls},
                                                           xr, (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
             }
-            // GRU1's per-unit constants (v = W_ih1 w0, w0; L1/L2-resident), fetched here rather
-            // than held in registers across the step: they land while the candidates arrive
-            float vj0 = 0.f, vj1 = 0.f, vj2 = 0.f, w0u = 0.f;
-            if (cell) {
-                int uu = cu;
-                asm volatile("" : "+v"(uu));
-                const rsrc_t vr = mk_rsrc(a.v);
-                vj0 = bld(vr, (unsigned)uu * 4u, 0);
-                vj1 = bld(vr, (unsigned)(kPH + uu) * 4u, 0);
-                vj2 = bld(vr, (unsigned)(2 * kPH + uu) * 4u, 0);
-                w0u = bld(mk_rsrc(a.w0), (unsigned)uu * 4u, 0);
-            }
             // ============= hop D: sample of step t, per cell wave for its own 4 rows ========
             // lane (row cn, cul) reads the candidates of slots 2 cul, 2 cul + 1 of its row; the
             // row's 16 lanes reduce them (DPP), so every cell of the row holds the sample
@@ -588,14 +573,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
         } else {
-            // waves 4-7: P1(t + 2) of cell i = tid - 256 (the cell of thread i of waves 0-3)
-            // into WL_P1, then the wave's tag. WL_P1 overlays the W_hh1 h1 partials, dead from
-            // their last read (fc1 epilogue window) to the next step's stage-A barrier; waves
-            // 0-3 read it before that barrier.
+            // waves 4-7: ring entry of step t + 3 for cell i = tid - 256 (written three steps
+            // ahead: its stores are drained by this wave's next poll, before the next stage-A
+            // barrier, and waves 0-3 read it two steps later; slot (t + 3) & 3 last held step
+            // t - 1, whose reads ended in step t - 1)
             const int i = tid - 256;
-            if (WRNN_WIDE_P1X && i < 16 * R) reinterpret_cast<float4*>(lds + WL_P1)[i] = p1_make(i >> 4, 16 * w + (i & 15), t + 2);
-            asm volatile("" ::: "memory");  // the tag after the wave's P1 store (LDS in order)
-            if (l == 0) reinterpret_cast<volatile int*>(lds + WL_P1F)[v - 4] = t + 2;
+            if (i < 16 * R) ring_make(i >> 4, 16 * w + (i & 15), t + 3);
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
@@ -611,6 +594,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 
 size_t persist_wide_lds_bytes() { return (size_t)WL_TOTAL * sizeof(float); }
 size_t persist_wide_xbuf_floats() { return (size_t)kPG * WX_GROUP; }
+size_t persist_wide_ring_floats() { return (size_t)kPG * WR_GROUP; }
 size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
 size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
 
@@ -622,7 +606,7 @@ int persist_wide_scratch() {
 
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > kPM * 16 ||
-        a.mode != 0 || a.wwide == nullptr)
+        a.mode != 0 || a.wwide == nullptr || a.wring == nullptr)
         return hipErrorInvalidValue;
     if (a.dbg.out) return persist_launch<k_persist_wide<true>>(persist_wide_lds_bytes(), a, s);
     return persist_launch<k_persist_wide<false>>(persist_wide_lds_bytes(), a, s);

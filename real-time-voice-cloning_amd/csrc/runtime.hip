@@ -206,7 +206,7 @@ struct wrnn_handle {
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
     } pw;
     struct PersistWS {
-        DevBuf P1, gumbel, ctl, xbuf, st, stamps, phases;
+        DevBuf P1, gumbel, ctl, xbuf, st, stamps, phases, wring;
     } pws;
     int engine = WRNN_ENGINE_AUTO;  // requested engine (wrnn_set_engine / env WRNN_ENGINE)
     int last_engine = WRNN_ENGINE_CHAIN;
@@ -1890,6 +1890,10 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int nb = (int)h->p_plan.size();
     a.wwide = (const float4*)W.wwide;
     a.wwide_lds = (const float4*)W.wwide_lds;
+    if (any_wide) {  // the wide kernel forms P1 and the noise in-kernel into this ring
+        CHECK(P.wring.alloc(persist_wide_ring_floats() * sizeof(float)));
+        a.wring = P.wring.f();
+    }
     if (cb && !h->prog_host) {  // progress word + abort word (kAbortWord), two cache lines
         HIPC(hipHostMalloc((void**)&h->prog_host, 128, hipHostMallocMapped | hipHostMallocCoherent));
         HIPC(hipHostGetDevicePointer((void**)&h->prog_dev, h->prog_host, 0));

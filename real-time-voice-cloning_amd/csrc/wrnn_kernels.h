@@ -236,6 +236,7 @@ struct PersistArgs {
     // wide-row launches (kernels_persist_wide.hip): MFMA A-operand weight images
     const float4* wwide;    // [kPM][8 waves][40 float4][64 lanes]
     const float4* wwide_lds;// [kPM][2 tiles][8][4][64] (W_hh2 z, n)
+    float* wring;           // wide launches: per-group ring of P1 and noise (persist_wide_ring_floats)
     DbgLogits dbg;
 };
 
@@ -246,6 +247,7 @@ constexpr int kPWideRows = 16;
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
 size_t persist_wide_lds_bytes();
 size_t persist_wide_xbuf_floats();
+size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
 int persist_wide_scratch();
