@@ -14,13 +14,14 @@
 //  * GRU1 distributed, not redundant: each slot runs GRU1 for its own 16 units x rows and
 //    publishes x1 / h1 (redundant GRU1 of all 512 units would cost 16x the cell work here).
 //    Five in-group hops per step: E (x1, h1), A (x2, h2), B (y1), C (y2), D (fc3 candidates).
-//  * Exchange: every published vector is laid out as 16-byte couples {v(u), tag, v(u+1), tag}
-//    in MFMA B-operand order ([wave e][couple i][k-slot c][row n]), so a consumer wave reads its
-//    B operand straight into registers with 8 fully coalesced 1-KiB loads per hop and checks
-//    the step tags itself -- no LDS staging of activations, no flags. Producers store with
-//    plain vector stores; consumers load non-temporal (L2-served): both ends of every hop are
-//    on one XCD (HW_REG_XCC_ID grouping), so the XCD's L2 is the coherence point (DESIGN.md §3,
-//    "Memory ordering").
+//  * Exchange: every published vector is laid out as 16-byte packets of 4 floats in MFMA
+//    B-operand order, two slots by step parity, so a consumer wave reads its B operand straight
+//    into registers with 4 fully coalesced 1-KiB loads per hop. Untagged: the slot a producer
+//    will write next holds a sentinel (see w_poll for why that is race-free), so a hop moves
+//    4 B per value (a tagged pair moved 8) -- no LDS staging of activations, no flags.
+//    Producers store with plain vector stores; consumers load non-temporal (L2-served): both
+//    ends of every hop are on one XCD (HW_REG_XCC_ID grouping), so the XCD's L2 is the
+//    coherence point ("Memory ordering").
 //  * Off-path products (W_hh1 h1 -> gh1, W_hh2 h2 -> gh2 of the next step) run in the waits of
 //    hops A and B; waves 4-7 (no epilogue cells) start them while waves 0-3 run the epilogues.
 // Every spin is bounded; on a timeout / error the kernel sets PC_ERR and every wave exits at
@@ -34,7 +35,16 @@ namespace wrnn {
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 // ---- exchange area per group (floats) ---------------------------------------------------
-constexpr int WV = 8 * 8 * 4 * 16 * 4;  // one vector buffer: [e 8][i 8][c 4][n 16] couples
+// One published vector (x1, h1, x2, h2, y1, y2) per step: two slots (step parity), each
+// [e 8][p 4][lane 64] packets of 4 floats in MFMA B-operand order -- packet p of consumer lane
+// l = 16 c + n of wave e holds row n, units 64 e + 16 c + 4 p + q (q = 0..3), i.e. the B operands
+// of k-steps 4p..4p+3 (k-step ks of k-slot c is unit 64 e + 16 c + ks: the weight images' order,
+// runtime.hip pack_persist_wide) -- then room for 1024 more floats. Untagged: a slot not yet written for
+// the step holds the sentinel kSent (see pub / w_poll).
+constexpr int WS_MAIN = 8 * 4 * 64 * 4;
+constexpr int WSLOT = WS_MAIN + 1024;
+constexpr int WV = 2 * WSLOT;
+constexpr unsigned kSent = 0x7fbadbadu;  // a signalling NaN: no arithmetic result is ever this
 enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
 constexpr int WX_D = WB_N * WV;                    // candidates [n 16][slot 32] (value, tag|class)
 constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
@@ -75,9 +85,13 @@ __device__ __forceinline__ v4f mfma4(float a, float b, v4f c) {
 __device__ __forceinline__ float f4c(const float4& q, int i) {
     return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w;
 }
-// B operand of k-step ks from the 8 couples of a hop (couple i holds k-steps 2i, 2i + 1)
-__device__ __forceinline__ float bop(const u4v (&cc)[8], int ks) {
-    return __uint_as_float((ks & 1) ? cc[ks >> 1].z : cc[ks >> 1].x);
+// B operand of k-step ks from the 4 packets of a hop (packet p holds k-steps 4p .. 4p + 3)
+__device__ __forceinline__ float bop(const u4v (&cc)[4], int ks) {
+    const u4v& q = cc[ks >> 2];
+    return __uint_as_float((ks & 3) == 0 ? q.x : (ks & 3) == 1 ? q.y : (ks & 3) == 2 ? q.z : q.w);
+}
+__device__ __forceinline__ bool p_ready(const u4v& q) {
+    return q.x != kSent && q.y != kSent && q.z != kSent && q.w != kSent;
 }
 
 // LDS-only workgroup barrier: no wait on outstanding global loads (prefetches stay in flight)
@@ -85,41 +99,47 @@ __device__ __forceinline__ void wbar() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Poll this lane's 8 couples of one hop buffer (byte offset of couple 0: voff; couple i at
-// voff + 1 KiB i) until all 16 tags equal `want`: spin on couple 0, then load the rest and
-// verify. Lanes with valid == false (rows beyond the group's count) contribute zeros.
-__device__ __forceinline__ bool w_poll8(rsrc_t xr, unsigned voff, unsigned so, unsigned want,
-                                        bool valid, u4v (&cc)[8], unsigned* ctl) {
+// Poll this lane's 4 packets of one hop buffer slot (byte offset of packet 0: voff; packet p at
+// voff + 1 KiB p; so: the buffer and slot) until no value is the sentinel: all 4 in flight at
+// first (the data is often there already), then spin on packet 0 and reload the rest. Lanes
+// with valid == false (rows beyond the group's count) contribute zeros.
+// Why a sentinel is enough (no step tags): a producer writes step s into slot s & 1 and the
+// sentinel into slot (s + 1) & 1 (pub). Its next poll waits for every older vector memory
+// operation of the wave (vmcnt counts stores on gfx9), so that reset is in L2 before it
+// publishes anything later; a consumer polls slot (s + 1) & 1 for step s + 1 only after it has
+// read such a later publication, so it sees the reset or the new value, never step s - 1. And
+// slot s & 1 is rewritten (step s + 2) only after every consumer has published past its reads
+// of step s.
+__device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4],
+                                       unsigned* ctl) {
     const unsigned t0 = p_now();
     unsigned nsp = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cc[i] = (u4v){0u, want, 0u, want};
+    for (int i = 0; i < 4; ++i) cc[i] = (u4v){0u, 0u, 0u, 0u};
     {
-        // first pass: all 8 couples in flight at once -- the data is often there already
-        // (one L2 round trip instead of two); then spin on couple 0 as below
         bool ok = true;
         if (valid) {
             unsigned vo = voff;
             asm volatile("" : "+v"(vo));
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+            for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) ok = ok && cc[i].y == want && cc[i].w == want;
+            for (int i = 0; i < 4; ++i) ok = ok && p_ready(cc[i]);
         }
         if (__all(ok)) return true;
     }
     while (true) {
         if (valid) cc[0] = __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, kCpNT);
-        if (__all(cc[0].y == want && cc[0].w == want)) {
+        if (__all(!valid || p_ready(cc[0]))) {
             bool ok = true;
             if (valid) {
                 unsigned vo = voff;
                 asm volatile("" : "+v"(vo));  // (offsets recomputed per use: hoisted ones pin registers)
 #pragma unroll
-                for (int i = 1; i < 8; ++i)
+                for (int i = 1; i < 4; ++i)
                     cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
 #pragma unroll
-                for (int i = 1; i < 8; ++i) ok = ok && cc[i].y == want && cc[i].w == want;
+                for (int i = 1; i < 4; ++i) ok = ok && p_ready(cc[i]);
             }
             if (__all(ok)) return true;
         }
@@ -206,15 +226,23 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         const int idx = tid < 96 ? (k / 16) * kPH + 16 * w + (k & 15) : 16 * w + k;
         lds[WL_BIAS + tid] = tid >= 96 && 16 * w + k >= a.n_classes ? 0.f : src[idx];
     }
-    // byte offsets: this lane's couple 0 in a hop buffer (consumer); the cell pair's couple
-    // (producer: even units publish the pair {u, u + 1})
-    const unsigned o_cons = (unsigned)((v * 8 * 64 + l) * 16);
-    const unsigned o_prod = (unsigned)(((((w >> 2) * 8 + (cul >> 1)) * 4 + (w & 3)) * 16 + cn) * 16);
-    auto pub = [&](int hb, float val, unsigned tag) {
-        const float nb = pdpp<0xB1>(val);  // unit u ^ 1 of the same row (quad_perm xor 1)
-        if (cell && (cul & 1) == 0)
-            __builtin_amdgcn_raw_buffer_store_b128((u4v){__float_as_uint(val), tag, __float_as_uint(nb), tag},
-                                                   xr, o_prod, (unsigned)(hb * WV) * 4u, 0);
+    // byte offsets in a slot: this lane's packet 0 (consumer); the packet of the unit quad
+    // cul .. cul + 3 of row cn (producer: lane cul % 4 == 0 of the quad gathers and publishes;
+    // slot w = wave e = w / 4, k-slot c = w % 4, packet p = cul / 4)
+    const unsigned o_cons = (unsigned)((v * 4 * 64 + l) * 16);
+    const unsigned o_prod = (unsigned)((((w >> 2) * 4 + (cul >> 2)) * 64 + 16 * (w & 3) + cn) * 16);
+    // publish the cell's value of step s: slot s & 1, and the sentinel into slot (s + 1) & 1
+    auto pub = [&](int hb, float val, unsigned s) {
+        // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]: quad lane 0 receives lanes 1, 2, 3
+        const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
+        if (cell && (cul & 3) == 0) {
+            const unsigned sb = (unsigned)(hb * WV) * 4u;
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr, o_prod,
+                sb + (s & 1u) * (unsigned)WSLOT * 4u, 0);
+            __builtin_amdgcn_raw_buffer_store_b128((u4v){kSent, kSent, kSent, kSent}, xr, o_prod,
+                                                   sb + ((s + 1u) & 1u) * (unsigned)WSLOT * 4u, 0);
+        }
     };
     const rsrc_t fcr = mk_rsrc(a.fcond);
     const rsrc_t rr = mk_rsrc(a.wring + (size_t)g * WR_GROUP);  // this group's operand ring
@@ -308,20 +336,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    // initial hop E: x1, h1 of step t0 (k_persist_init) with tag t0 + 1
-    pub(WB_X1, cell ? lds[WL_X1 + cn * 16 + cul] : 0.f, (unsigned)a.t0 + 1u);
-    pub(WB_H1, h1r, (unsigned)a.t0 + 1u);
-    const unsigned so_x1 = (unsigned)(WB_X1 * WV) * 4u, so_h1 = (unsigned)(WB_H1 * WV) * 4u;
-    const unsigned so_x2 = (unsigned)(WB_X2 * WV) * 4u, so_h2 = (unsigned)(WB_H2 * WV) * 4u;
-    const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u, so_y2 = (unsigned)(WB_Y2 * WV) * 4u;
+    // initial hop E: x1, h1 of step t0 (k_persist_init) as step t0 + 1 (canonicalised: a
+    // signalling NaN in a carried state must not read as the sentinel)
+    pub(WB_X1, __builtin_canonicalizef(cell ? lds[WL_X1 + cn * 16 + cul] : 0.f), (unsigned)a.t0 + 1u);
+    pub(WB_H1, __builtin_canonicalizef(h1r), (unsigned)a.t0 + 1u);
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
         const unsigned seq = (unsigned)t + 1u;
-        u4v cc[8];
+        const unsigned slot = (seq & 1u) * (unsigned)WSLOT * 4u;
+        const unsigned so_x1 = (unsigned)(WB_X1 * WV) * 4u + slot, so_h1 = (unsigned)(WB_H1 * WV) * 4u + slot;
+        const unsigned so_x2 = (unsigned)(WB_X2 * WV) * 4u + slot, so_h2 = (unsigned)(WB_H2 * WV) * 4u + slot;
+        const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u + slot, so_y2 = (unsigned)(WB_Y2 * WV) * 4u + slot;
+        u4v cc[4];
         bool fail = false;
         WSTAMP(0);
         // ================= hop E -> stage A: W_ih2[:, :512] x1 (critical) ==================
-        fail |= !w_poll8(xr, o_cons, so_x1, seq, bvalid, cc, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_x1, bvalid, cc, a.ctl);
         prefetch(t);
         WSTAMP(1);
         {
@@ -362,7 +392,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         WSTAMP(3);
         // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
         {
-            fail |= !w_poll8(xr, o_cons, so_h1, seq, bvalid, cc, a.ctl);
+            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl);
             WXSTAMP(26);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -377,7 +407,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
-        fail |= !w_poll8(xr, o_cons, so_x2, seq, bvalid, cc, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl);
         WSTAMP(4);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -418,7 +448,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
             WXSTAMP(28);
-            fail |= !w_poll8(xr, o_cons, so_h2, seq, bvalid, cc, a.ctl);
+            fail |= !w_poll(xr, o_cons, so_h2, bvalid, cc, a.ctl);
             WXSTAMP(29);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -440,7 +470,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WXSTAMP(30);
         // ================= hop B -> stage C: fc2 y1 (critical) =============================
-        fail |= !w_poll8(xr, o_cons, so_y1, seq, bvalid, cc, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_y1, bvalid, cc, a.ctl);
         WSTAMP(6);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -478,7 +508,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 }
         }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
-        fail |= !w_poll8(xr, o_cons, so_y2, seq, bvalid, cc, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl);
         WSTAMP(8);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -594,6 +624,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 
 size_t persist_wide_lds_bytes() { return (size_t)WL_TOTAL * sizeof(float); }
 size_t persist_wide_xbuf_floats() { return (size_t)kPG * WX_GROUP; }
+// before every wide launch: the vector slots to the sentinel, the candidate area (step tags) to 0
+__global__ __launch_bounds__(256) void k_wide_xbuf_reset(uint4* x) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)kPG * WX_GROUP / 4) return;
+    const unsigned f = (unsigned)((i * 4) % WX_GROUP);
+    x[i] = f >= (unsigned)WX_D ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(kSent, kSent, kSent, kSent);
+}
+static_assert(WX_GROUP % 4 == 0 && WX_D % 4 == 0, "reset works in 16-byte units");
+hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s) {
+    const unsigned n = (unsigned)((size_t)kPG * WX_GROUP / 4);
+    k_wide_xbuf_reset<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<uint4*>(xbuf));
+    return hipGetLastError();
+}
 size_t persist_wide_ring_floats() { return (size_t)kPG * WR_GROUP; }
 size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
 size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }

@@ -1917,7 +1917,10 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.t0 = 0;
         a.t1 = S;
         a.prog_base = b * S;
-        HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
+        if (L.wide)  // sentinel-initialised vector slots (kernels_persist_wide.hip w_poll)
+            HIPC(persist_wide_reset_xbuf(P.xbuf.f(), st));
+        else
+            HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
         // registration words only: an error code from an earlier launch stays visible, so the
         // later launches of a failed call exit at registration (p_register)
         HIPC(hipMemsetAsync(P.ctl.p, 0, PC_ERR * sizeof(unsigned), st));

@@ -247,6 +247,7 @@ constexpr int kPWideRows = 16;
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
 size_t persist_wide_lds_bytes();
 size_t persist_wide_xbuf_floats();
+hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s);
 size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
