@@ -58,11 +58,8 @@ constexpr int WR_GROUP = WR_G + WR_SLOTS * 16 * kPH;
 // ---- LDS (floats) -------------------------------------------------------------------------
 // Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
 // the instruction's 16-bit immediate (beyond it each access would pin an address register).
-constexpr int WL_GH1 = 0;                        // gh1 of the slot's units [3][16 n][16 ul]
-constexpr int WL_GH2 = WL_GH1 + 768;             // gh2 [3][16 n][16 ul]
-constexpr int WL_X1 = WL_GH2 + 768;              // x1 of the slot's units [16 n][16 ul]
-constexpr int WL_RI = WL_X1 + 256;               // RowInfo of the group's rows (6 words each)
-constexpr int WL_FAIL = WL_RI + 16 * 6;
+constexpr int WL_RI = 0;                         // RowInfo of the group's rows (6 words each)
+constexpr int WL_FAIL = WL_RI + 128;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
@@ -71,7 +68,7 @@ constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layo
 constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(WL_BIAS + 112 <= WL_PS, "small LDS arrays overflow their 8 KiB");
+static_assert(WL_BIAS + 112 <= 256, "small LDS arrays overflow their 1 KiB");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -203,7 +200,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #define WR(T, ks) f4c(wq[4 * (T) + (ks) / 4], (ks) % 4)
     const float4* hh2 = reinterpret_cast<const float4*>(lds + WL_HH2);
     // ---- state and per-cell constants --------------------------------------------------
-    float h1r = 0.f, h2r = 0.f, vj0 = 0.f, vj1 = 0.f, vj2 = 0.f, w0u = 0.f;
+    // cell state in registers: h1, h2, x1 and gh2 = W_hh2 h2 + b_hh2 of the next GRU2 (the
+    // epilogue lanes sum the gh partials themselves, in the hop D wait)
+    float h1r = 0.f, h2r = 0.f, vj0 = 0.f, vj1 = 0.f, vj2 = 0.f, w0u = 0.f, x1c = 0.f;
+    float g1r = 0.f, g1z = 0.f, g1n = 0.f, g2r = 0.f, g2z = 0.f, g2n = 0.f;
     if (cell) {
         vj0 = a.v[cu];
         vj1 = a.v[kPH + cu];
@@ -211,10 +211,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         w0u = a.w0[cu];
         h1r = a.st_h1[(size_t)crow * kPH + cu];
         h2r = a.st_h2[(size_t)crow * kPH + cu];
-        lds[WL_X1 + cn * 16 + cul] = a.st_x1[(size_t)crow * kPH + cu];
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            lds[WL_GH2 + (j * 16 + cn) * 16 + cul] = a.st_gh2[(size_t)crow * 3 * kPH + j * kPH + cu];
+        x1c = a.st_x1[(size_t)crow * kPH + cu];
+        g2r = a.st_gh2[(size_t)crow * 3 * kPH + cu];
+        g2z = a.st_gh2[(size_t)crow * 3 * kPH + kPH + cu];
+        g2n = a.st_gh2[(size_t)crow * 3 * kPH + 2 * kPH + cu];
     }
     if (tid < R) reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
     if (tid == 0) lds[WL_FAIL] = 0.f;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     __syncthreads();
     // initial hop E: x1, h1 of step t0 (k_persist_init) as step t0 + 1 (canonicalised: a
     // signalling NaN in a carried state must not read as the sentinel)
-    pub(WB_X1, __builtin_canonicalizef(cell ? lds[WL_X1 + cn * 16 + cul] : 0.f), (unsigned)a.t0 + 1u);
+    pub(WB_X1, __builtin_canonicalizef(x1c), (unsigned)a.t0 + 1u);
     pub(WB_H1, __builtin_canonicalizef(h1r), (unsigned)a.t0 + 1u);
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
@@ -382,9 +382,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + cn) * 16 + cul];
                     gi[j] = p_add(s, pc[j]);
                 }
-                const float* gh = lds + WL_GH2 + cn * 16 + cul;
-                h2r = p_gru(gi[0], gi[1], gi[2], gh[0], gh[256], gh[512], h2r);
-                x2 = p_add(lds[WL_X1 + cn * 16 + cul], h2r);
+                h2r = p_gru(gi[0], gi[1], gi[2], g2r, g2z, g2n, h2r);
+                x2 = p_add(x1c, h2r);
             }
             pub(WB_X2, x2, seq);
             pub(WB_H2, h2r, seq);
@@ -433,17 +432,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 y = y > 0.f ? y : 0.f;
             }
             pub(WB_Y1, y, seq);
-        } else {  // gh1 = sum of the W_hh1 h1 partials + b_hh1 (waves 4-7; read by GRU1)
-            const int i = tid - 256, rn = i >> 4, ul = i & 15;
-            if (rn < R)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PH + ((vv * 3 + j) * 16 + rn) * 16 + ul];
-                    lds[WL_GH1 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, lds[WL_BIAS + j * 16 + ul]);
-                }
         }
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
@@ -495,17 +483,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 y = y > 0.f ? y : 0.f;
             }
             pub(WB_Y2, y, seq);
-        } else {  // gh2 of the next step = sum of the W_hh2 h2 partials + b_hh2 (waves 4-7)
-            const int i = tid - 256, rn = i >> 4, ul = i & 15;
-            if (rn < R)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + rn) * 16 + ul];
-                    lds[WL_GH2 + (j * 16 + rn) * 16 + ul] =
-                        p_add(s, lds[WL_BIAS + 48 + j * 16 + ul]);
-                }
         }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
         fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl);
@@ -542,6 +519,27 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 if (cell && cul == 0)
                     __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls},
                                                           xr, (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
+            }
+            // gh1 = W_hh1 h1 + b_hh1 (for GRU1 below) and gh2 = W_hh2 h2 + b_hh2 (the next GRU2)
+            // from the off-path partials, while the candidates travel: every wave wrote them
+            // before the stage C barrier, and they are rewritten only after this workgroup's
+            // x1 publish (PH: next hop A wait; PA: next stage A, behind the x1 hop)
+            if (cell) {
+                float gs[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int vv = 0; vv < 8; ++vv)
+                        s += lds[(j < 3 ? WL_PH : WL_PA) + ((vv * 3 + j % 3) * 16 + cn) * 16 + cul];
+                    gs[j] = p_add(s, lds[WL_BIAS + 16 * j + cul]);
+                }
+                g1r = gs[0];
+                g1z = gs[1];
+                g1n = gs[2];
+                g2r = gs[3];
+                g2z = gs[4];
+                g2n = gs[5];
             }
             // ============= hop D: sample of step t, per cell wave for its own 4 rows ========
             // lane (row cn, cul) reads the candidates of slots 2 cul, 2 cul + 1 of its row; the
@@ -594,11 +592,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // (at the last step it runs on clamped inputs and nobody reads the result)
             float x1 = 0.f;
             if (cell) {
-                const float* gh = lds + WL_GH1 + cn * 16 + cul;
-                h1r = p_gru(fmaf(vj0, x, pp.x), fmaf(vj1, x, pp.y), fmaf(vj2, x, pp.z), gh[0], gh[256],
-                            gh[512], h1r);
+                h1r = p_gru(fmaf(vj0, x, pp.x), fmaf(vj1, x, pp.y), fmaf(vj2, x, pp.z), g1r, g1z, g1n, h1r);
                 x1 = p_add(fmaf(w0u, x, pp.w), h1r);
-                lds[WL_X1 + cn * 16 + cul] = x1;
+                x1c = x1;
             }
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
