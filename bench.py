@@ -366,6 +366,12 @@ def main():
             roof['traffic'] = pmc['traffic_bytes']
             roof['traffic_source'] = pmc['source']
             roof['traffic_note'] = pmc['correction']
+            # counter-backed utilisation of the same kernel (SQ pass, tools/pmc_traffic.py):
+            # MFMA pipe busy fraction over all 1024 SIMDs, LDS bank-conflict share, wave states
+            for k in ('mfma_busy_frac', 'lds_conflict_frac', 'wait_frac', 'issue_stall_frac',
+                      'active_frac', 'sq_source'):
+                if k in pmc:
+                    roof[k] = pmc[k]
     fb = model.fallback_info()
     result = {
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',

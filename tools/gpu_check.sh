@@ -20,6 +20,7 @@ STEPS=${STEPS:-parity,smoke,bench}
 [[ ,$STEPS, == *,phase,* ]] && run phase 300 env WRNN_PHASE_STEP=${PHASE_STEP:-600} python bench.py --steps 1 --warmup 0 --cpu-seconds 0
 [[ ,$STEPS, == *,smoke,* ]] && run smoke 300 python __graft_entry__.py smoke
 [[ ,$STEPS, == *,bench,* ]] && run bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds ${CPU_SECONDS:-10}
+[[ ,$STEPS, == *,bench_c4,* ]] && run bench_c4 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
 [[ ,$STEPS, == *,rehearse,* ]] && run rehearse 600 env WRNN_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 1 --warmup 1 --cpu-seconds ${CPU_SECONDS:-10}
 [[ ,$STEPS, == *,prof,* ]] && run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-timing
 exit 0

@@ -1,10 +1,21 @@
-"""Fold the FETCH_SIZE / WRITE_SIZE passes of tools/measure.sh into profiles/pmc_traffic.json,
-which bench.py reads for roofline.traffic (rocprofv3 cannot run inside the bench process).
+"""Fold rocprofv3 counter passes into profiles/pmc_traffic.json, which bench.py reads for
+roofline.traffic and the counter-backed fractions (rocprofv3 cannot run inside the bench process).
 
-usage: python tools/pmc_traffic.py gpurun_out/measure profiles/<round dir>
-Copies the counter CSVs to <round dir>/pmc/ and writes one entry per topology, keyed
-'k_persist|<bench workload string>'.
+usage: python tools/pmc_traffic.py <pass dir> <round dir> [bench args note]
+  <pass dir>: tools/pmc_r03.sh output (gpurun_out/pmc3): <w>_fetch/, <w>_write/, <w>_sq/ per
+              workload w (c2, c4, ...), each with run_counter_collection.csv
+Copies the CSVs to <round dir>/pmc/ and writes one entry per workload, keyed
+'<kernel>|<bench workload string>', with per-launch values of the dominant kernel:
+  traffic_bytes   HBM bytes: FETCH_SIZE x 2 + WRITE_SIZE (KiB counters; MI355X_MICROARCH.md HBM
+                  section: gfx950 FETCH_SIZE tallies the 128-B requests of coalesced reads at 64 B)
+  mfma_busy_frac  SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel cycles =
+                  GRBM_GUI_ACTIVE / 8 (GRBM is summed over the 8 XCDs); the busy counter counts
+                  MFMA pipe cycles (32 per v_mfma_f32_16x16x4_f32, MI355X_MICROARCH.md)
+  lds_conflict_frac  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles / all LDS cycles)
+  wait_frac, issue_stall_frac, active_frac  SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY
+                  over SQ_WAVE_CYCLES (disjoint, MI355X_MICROARCH.md PMC table)
 """
+import collections
 import csv
 import json
 import os
@@ -14,32 +25,43 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CORR = ("FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE tallies the 128-B "
-        "memory requests of coalesced reads at 64 B); the dominant stream is the [S][B][4H] P1 "
-        "stream (16-B loads) for k_persist_wide / k_persist_rr / k_persist_gen and, for k_persist "
-        "(P1 formed in-kernel), the Gumbel noise (4-B lane loads, 256 B per wave) plus the per-frame "
-        "tables; WRITE_SIZE as reported")
-# workload -> (bench.py arguments as in tools/measure.sh ARGS, bench workload string, kernel key)
+        "memory requests of coalesced reads at 64 B); WRITE_SIZE as reported")
+N_SIMD = 1024
+
+
 def workload(model, wname, frames=1000, utts=1, target=11000, overlap=550):
     return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
             f'batched folds target={target} overlap={overlap}')
 
 
+# workload -> (bench.py arguments as in tools/pmc_r03.sh ARGS, bench workload string, kernel)
 WORKLOADS = {
     'c2': ('', workload('fatchord-wavernn', 'RAW 9-bit mu-law'), 'k_persist'),
     'c4': (' --utts-per-gpu 8', workload('fatchord-wavernn', 'RAW 9-bit mu-law', utts=8), 'k_persist_wide'),
     'c3': (' --mode MOL', workload('fatchord-wavernn', 'MOL'), 'k_persist'),
-    'rr': (' --model runtimeracer-wavernn --bits 9', workload('runtimeracer-wavernn', 'RAW 9-bit mu-law'),
-           'k_persist'),
-    'gen': (' --model geneing-wavernn --mode BITS --bits 10', workload('geneing-wavernn', 'BITS 10-bit'),
-            'k_persist'),
 }
 
 
-def counter(path, kernel):
-    def base(name):  # 'void wrnn::k_persist<3, false>(wrnn::PersistArgs)' -> 'k_persist'
-        return name.split('(')[0].split('<')[0].split('::')[-1]
-    rows = [r for r in csv.DictReader(open(path)) if base(r['Kernel_Name']) == kernel]
-    return rows[0]['Kernel_Name'], sum(float(r['Counter_Value']) for r in rows), len(rows)
+def base(name):  # 'void wrnn::k_persist<3, false>(wrnn::PersistArgs)' -> 'k_persist'
+    return name.split('(')[0].split('<')[0].split('::')[-1]
+
+
+def per_launch(path, kernel):
+    """{counter: value per launch} of `kernel` (summed over the dimension rows of a dispatch,
+    averaged over dispatches), its full name and the dispatch count."""
+    disp = collections.defaultdict(lambda: collections.defaultdict(float))
+    name = None
+    for r in csv.DictReader(open(path)):
+        if base(r['Kernel_Name']) != kernel:
+            continue
+        name = r['Kernel_Name']
+        disp[r['Dispatch_Id']][r['Counter_Name']] += float(r['Counter_Value'])
+    n = len(disp)
+    tot = collections.defaultdict(float)
+    for c in disp.values():
+        for k, v in c.items():
+            tot[k] += v
+    return {k: v / n for k, v in tot.items()}, name, n
 
 
 def main():
@@ -48,25 +70,40 @@ def main():
     jpath = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     table = json.load(open(jpath)) if os.path.exists(jpath) else {}
     for key, (extra, wl, kernel) in WORKLOADS.items():
-        f = os.path.join(src, f'pmc_fetch_{key}', 'run_counter_collection.csv')
-        w = os.path.join(src, f'pmc_write_{key}', 'run_counter_collection.csv')
-        if not (os.path.exists(f) and os.path.exists(w)):
+        paths = {p: os.path.join(src, f'{key}_{p}', 'run_counter_collection.csv')
+                 for p in ('fetch', 'write', 'sq')}
+        if not (os.path.exists(paths['fetch']) and os.path.exists(paths['write'])):
             continue
-        kname, fetch, n = counter(f, kernel)
-        _, write, _ = counter(w, kernel)
-        dst_f = os.path.join(out, 'pmc', f'fetch_size_{key}.csv')
-        dst_w = os.path.join(out, 'pmc', f'write_size_{key}.csv')
-        shutil.copy(f, dst_f)
-        shutil.copy(w, dst_w)
-        traffic = (2 * fetch + write) * 1024.0 / n  # KiB counters, per launch
-        table[f'{kernel}|{wl}'] = {
-            'kernel': kname, 'launches': n, 'fetch_size_kib': fetch / n, 'write_size_kib': write / n,
-            'traffic_bytes': traffic, 'correction': CORR,
-            'source': f'{os.path.relpath(dst_f, REPO)}, {os.path.relpath(dst_w, REPO)}: rocprofv3 '
-                      f'--pmc FETCH_SIZE | WRITE_SIZE (separate passes) --kernel-include-regex '
-                      f'{kernel} -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 '
-                      f'--no-timing{extra}'}
-        print(key, kname, f'{traffic / 1e9:.3f} GB per launch')
+        for p, f in paths.items():
+            if os.path.exists(f):
+                shutil.copy(f, os.path.join(out, 'pmc', f'{key}_{p}.csv'))
+        fetch, kname, n = per_launch(paths['fetch'], kernel)
+        write, _, _ = per_launch(paths['write'], kernel)
+        traffic = (2 * fetch['FETCH_SIZE'] + write['WRITE_SIZE']) * 1024.0
+        rel = os.path.relpath(os.path.join(out, 'pmc'), REPO)
+        e = {'kernel': kname, 'launches': n, 'fetch_size_kib': fetch['FETCH_SIZE'],
+             'write_size_kib': write['WRITE_SIZE'], 'traffic_bytes': traffic, 'correction': CORR,
+             'source': f'{rel}/{key}_fetch.csv, {rel}/{key}_write.csv: rocprofv3 --pmc FETCH_SIZE | '
+                       f'WRITE_SIZE (separate passes) --kernel-include-regex {kernel} -- python3 '
+                       f'bench.py --steps 2 --warmup 1 --cpu-seconds 0 --no-timing{extra}'}
+        if os.path.exists(paths['sq']):
+            sq, _, _ = per_launch(paths['sq'], kernel)
+            cyc = sq['GRBM_GUI_ACTIVE'] / 8.0
+            wc = sq['SQ_WAVE_CYCLES']
+            e['counters'] = {k: sq[k] for k in sorted(sq)}
+            e['kernel_cycles'] = cyc
+            e['mfma_busy_frac'] = sq['SQ_VALU_MFMA_BUSY_CYCLES'] / (N_SIMD * cyc)
+            e['lds_conflict_frac'] = (sq['SQ_LDS_BANK_CONFLICT'] / sq['SQ_LDS_IDX_ACTIVE']
+                                      if sq['SQ_LDS_IDX_ACTIVE'] else 0.0)
+            e['wait_frac'] = sq['SQ_WAIT_ANY'] / wc
+            e['issue_stall_frac'] = sq['SQ_WAIT_INST_ANY'] / wc
+            e['active_frac'] = sq['SQ_ACTIVE_INST_ANY'] / wc
+            e['sq_source'] = (f'{rel}/{key}_sq.csv: rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES '
+                              f'SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES '
+                              f'SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE (one pass)')
+        table[f'{kernel}|{wl}'] = e
+        print(key, kname, f'{traffic / 1e9:.3f} GB per launch',
+              {k: round(e[k], 3) for k in ('mfma_busy_frac', 'lds_conflict_frac', 'wait_frac') if k in e})
     json.dump(table, open(jpath, 'w'), indent=1)
 
 
