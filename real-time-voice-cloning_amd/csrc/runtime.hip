@@ -2170,13 +2170,16 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
             if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
             // (a variant with register spills is not used unless WRNN_WIDE_ALLOW_SCRATCH=1: A/B)
-            const bool scratch_ok = persist_wide_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
-            if (wmode && h->pw.wwide && scratch_ok) {
+            const bool any_scratch_ok = std::getenv("WRNN_WIDE_ALLOW_SCRATCH") != nullptr;
+            if (wmode && h->pw.wwide) {
                 if (wmode == 1) opts.clear();
                 // measured per step: 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows per
                 // group (the MFMA tiles cost the same for any row count; the exchanges and
-                // epilogues grow a little with the rows), fit 11.45 + 0.057 r
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 11.45 + 0.057 * r});
+                // epilogues grow a little with the rows), fit 11.45 + 0.057 r; 17-18 rows (the
+                // XV instance: two rows on the VALU beside the tiles) 12.6
+                for (int r = 1; r <= kPWideRows; ++r)
+                    if (persist_wide_scratch(r) == 0 || any_scratch_ok)
+                        opts.push_back({r, true, r > 16 ? 12.6 : 11.45 + 0.057 * r});
             }
         } else {
             // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us

@@ -243,7 +243,7 @@ struct PersistArgs {
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 // Wide-row fatchord launch: up to kPWideRows rows per XCD group (8 kPWideRows per launch),
 // fp32 MFMA products, RAW categorical with <= 512 classes.
-constexpr int kPWideRows = 16;
+constexpr int kPWideRows = 18;  // 16 MFMA columns + 2 VALU rows (kernels_persist_wide.hip XV)
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
 size_t persist_wide_lds_bytes();
 size_t persist_wide_xbuf_floats();
@@ -251,7 +251,7 @@ hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s);
 size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
-int persist_wide_scratch();
+int persist_wide_scratch(int nr);
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
 // ---------------------------------------------------------------------------------------
