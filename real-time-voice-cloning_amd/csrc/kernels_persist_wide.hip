@@ -30,39 +30,30 @@
 #include "persist_common.h"
 #include "philox.h"
 
-#ifndef WRNN_WIDE_SPLIT
-#define WRNN_WIDE_SPLIT 1
-#endif
-
 namespace wrnn {
 
 typedef float v4f __attribute__((ext_vector_type(4)));
-
-// Rows per group: 16 MFMA columns, and in the XV instance 2 more "V rows" (group rows 16, 17)
-// whose products run on the VALU (v_pk_fma_f32) in the gaps between the same waves' MFMAs, from
-// the same weight registers -- 144 rows per launch, C4's whole per-GPU batch in one launch.
-constexpr int kWRows = 18;
 
 // ---- exchange area per group (floats) ---------------------------------------------------
 // One published vector (x1, h1, x2, h2, y1, y2) per step: two slots (step parity), each
 // [e 8][p 4][lane 64] packets of 4 floats in MFMA B-operand order -- packet p of consumer lane
 // l = 16 c + n of wave e holds row n, units 64 e + 16 c + 4 p + q (q = 0..3), i.e. the B operands
 // of k-steps 4p..4p+3 (k-step ks of k-slot c is unit 64 e + 16 c + ks: the weight images' order,
-// runtime.hip pack_persist_wide) -- then the V rows, [row 16 + n'][unit] plain. Untagged: a slot
-// not yet written for the step holds the sentinel kSent (see pub / w_poll).
+// runtime.hip pack_persist_wide) -- then room for 1024 more floats. Untagged: a slot not yet written for
+// the step holds the sentinel kSent (see pub / w_poll).
 constexpr int WS_MAIN = 8 * 4 * 64 * 4;
-constexpr int WSLOT = WS_MAIN + 2 * kPH;
+constexpr int WSLOT = WS_MAIN + 1024;
 constexpr int WV = 2 * WSLOT;
 constexpr unsigned kSent = 0x7fbadbadu;  // a signalling NaN: no arithmetic result is ever this
 enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
-constexpr int WX_D = WB_N * WV;                    // candidates [n 18][slot 32] (value, tag|class)
-constexpr int WX_GROUP = WX_D + kWRows * 32 * 2 + 64;
+constexpr int WX_D = WB_N * WV;                    // candidates [n 16][slot 32] (value, tag|class)
+constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
 // Per-group operand ring (PersistArgs::wring, runtime.hip persist_wide_ring_floats): P1 (r, z, n of
 // W_ih1 (I c) + b_ih1, then I c + b_I) and the Gumbel noise of every cell for 4 steps,
 // [slot = step & 3][row n][unit / class], formed in-kernel three steps ahead (see the fc3 window)
 constexpr int WR_SLOTS = 4;
-constexpr int WR_G = WR_SLOTS * kWRows * kPH * 4;  // P1: float4 [4][18][512] at 0; noise: float [4][18][512]
-constexpr int WR_GROUP = WR_G + WR_SLOTS * kWRows * kPH;
+constexpr int WR_G = WR_SLOTS * 16 * kPH * 4;  // P1: float4 [4][16][512] at 0; noise: float [4][16][512]
+constexpr int WR_GROUP = WR_G + WR_SLOTS * 16 * kPH;
 
 // ---- LDS (floats) -------------------------------------------------------------------------
 // Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
@@ -71,16 +62,13 @@ constexpr int WL_RI = 0;                         // RowInfo of the group's rows 
 constexpr int WL_FAIL = WL_RI + 128;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
-// partial tiles, NRW = 16 or 18 rows (the V rows at n = 16, 17):
-constexpr int WL_PS = 256;                       // 1-tile partials [8 v][NRW n][16 o]
-template <int NRW> constexpr int wl_pa() { return WL_PS + 8 * NRW * 16; }  // 3-tile [8 v][3][NRW n][16 o]
-template <int NRW> constexpr int wl_ph() { return wl_pa<NRW>() + 8 * 3 * NRW * 16; }  // W_hh1 h1 (same)
-constexpr int WL_HH2 = 16384;                    // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
+constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
+constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
+constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
+constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(kWRows * 6 <= WL_FAIL - WL_RI, "RowInfo array overflows");
-static_assert(WL_BIAS + 112 <= WL_PS, "small LDS arrays overflow their 1 KiB");
-static_assert(wl_ph<kWRows>() + 8 * 3 * kWRows * 16 <= WL_HH2, "partial tiles overlap the W_hh2 tiles");
+static_assert(WL_BIAS + 112 <= 256, "small LDS arrays overflow their 1 KiB");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -99,7 +87,7 @@ __device__ __forceinline__ float bop(const u4v (&cc)[4], int ks) {
     const u4v& q = cc[ks >> 2];
     return __uint_as_float((ks & 3) == 0 ? q.x : (ks & 3) == 1 ? q.y : (ks & 3) == 2 ? q.z : q.w);
 }
-// Partial tiles: element (row n, column o) of a [NRW][16] tile sits at n * 16 + wsw(n, o), the
+// Partial tiles: element (row n, column o) of a [16][16] tile sits at n * 16 + wsw(n, o), the
 // 16-byte column slots XOR-swizzled by row: an MFMA lane's 16-byte store (row bn, columns
 // 4c .. 4c + 3) and the epilogue's row reads are then both conflict-free (a ds_write_b128 is
 // served 8 contiguous lanes at a time on 32 banks: unswizzled, rows 64 B apart put 8 rows on 2
@@ -127,22 +115,14 @@ __device__ __forceinline__ void wbar() {
 // read such a later publication, so it sees the reset or the new value, never step s - 1. And
 // slot s & 1 is rewritten (step s + 2) only after every consumer has published past its reads
 // of step s.
-// XV: lanes l < 32 also poll one packet of the V rows (vvalid: its row exists), into cv.
-template <bool XV>
+// On a timeout the first poller records its site in PC_WHERE (`where`: site << 28 | slot << 22 |
+// step; the wave is added here) and whether its packets were missing, for the error message.
 __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4],
-                                       bool vvalid, u4v& cv, unsigned* ctl) {
+                                       unsigned* ctl, unsigned where) {
     const unsigned t0 = p_now();
     unsigned nsp = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) cc[i] = (u4v){0u, 0u, 0u, 0u};
-    if (XV) cv = (u4v){0u, 0u, 0u, 0u};
-    // the V packet of lane l < 32: row 16 + l / 16, units 4 (l & 15) .. + 3 of the wave's K range
-    auto vo_v = [&]() {
-        const unsigned l = threadIdx.x & 63u;
-        unsigned vo = (unsigned)(WS_MAIN * 4) + (l >> 4) * (unsigned)(kPH * 4) + (threadIdx.x >> 6) * 256u + (l & 15u) * 16u;
-        asm volatile("" : "+v"(vo));
-        return vo;
-    };
     {
         bool ok = true;
         if (valid) {
@@ -150,13 +130,9 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
             asm volatile("" : "+v"(vo));
 #pragma unroll
             for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
-        }
-        if (XV && vvalid) cv = __builtin_amdgcn_raw_buffer_load_b128(xr, vo_v(), so, kCpNT);
-        if (valid) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) ok = ok && p_ready(cc[i]);
         }
-        if (XV && vvalid) ok = ok && p_ready(cv);
         if (__all(ok)) return true;
     }
     while (true) {
@@ -169,16 +145,20 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 #pragma unroll
                 for (int i = 1; i < 4; ++i)
                     cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
-            }
-            if (XV && vvalid) cv = __builtin_amdgcn_raw_buffer_load_b128(xr, vo_v(), so, kCpNT);
-            if (valid) {
 #pragma unroll
                 for (int i = 1; i < 4; ++i) ok = ok && p_ready(cc[i]);
             }
-            if (XV && vvalid) ok = ok && p_ready(cv);
             if (__all(ok)) return true;
         }
         if ((++nsp & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
+            if (!ld_sc1_u(ctl + PC_ERR)) {  // the first to time out records where
+                bool mok = true;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mok = mok && (!valid || p_ready(cc[i]));
+                const bool mbad = !__all(mok);
+                if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | ((threadIdx.x >> 6) << 19)) == 0u)
+                    ctl[PC_WHERE + 1] = mbad ? 1u : 0u;
+            }
             if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
             return false;
         }
@@ -186,17 +166,9 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 }
 
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-// XV: 17-18 rows per group -- rows 16, 17 ("V rows") on the VALU beside the MFMA tiles: their
-//     products are v_pk_fma_f32 chains over the same weight registers (lane (unit l & 15,
-//     k-slot l >> 4) sums its 16 k-steps, then the 4 k-slots are summed by shuffles and the 8
-//     waves in the epilogue, like the MFMA partials), their operands staged per wave in LDS as
-//     (row 16, row 17) pairs, their cells on wave 4 (lanes 0-31), whose ring entries waves 5-7
-//     take over.
-template <bool DBG, bool XV>
+template <bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
-    constexpr int NRW = XV ? kWRows : 16;  // row stride of the partial tiles
-    constexpr int WL_PA = wl_pa<NRW>(), WL_PH = wl_ph<NRW>();
     int* sreg = reinterpret_cast<int*>(lds + WL_REG);
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -211,19 +183,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(sreg[1]);
     const int v = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave: K-eighth [64v, 64v + 64)
     const int l = tid & 63;
-    const int R = a.nr;                  // rows of this group (<= 16; XV: 17, 18)
+    const int R = a.nr;                  // rows of this group (<= 16)
     const int g0 = a.rb + g;             // group row r = fold row g0 + 8 r
     const int bn = l & 15;               // B-operand lane: row bn, k-slot l >> 4
     const bool bvalid = bn < R;
-    const bool vvalid = XV && l < 32 && 16 + (l >> 4) < R;  // V packet lane (w_poll)
-    // epilogue cell of threads 0..16R-1: row cn, unit / class 16 w + cul (XV: rows 16, 17 on
-    // wave 4)
+    // epilogue cell of threads 0..16R-1: row cn, unit / class 16 w + cul
     const int cn = tid >> 4, cul = tid & 15;
     const bool cell = tid < 16 * R;
     const int cu = 16 * w + cul;
     const int crow = g0 + kPG * (cell ? cn : 0);
-    // waves holding epilogue cells: 0-3, and 4 in the XV instance
-    const bool cw = v < 4 || (XV && v == 4);
+    int t_now = 0;  // (for the timeout site record, PC_WHERE)
+    auto wh = [&](unsigned site) { return site << 28 | (unsigned)w << 22 | ((unsigned)t_now & 0x7ffffu); };
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * WX_GROUP);
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
@@ -276,9 +246,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     // cul .. cul + 3 of row cn (producer: lane cul % 4 == 0 of the quad gathers and publishes;
     // slot w = wave e = w / 4, k-slot c = w % 4, packet p = cul / 4)
     const unsigned o_cons = (unsigned)((v * 4 * 64 + l) * 16);
-    // (a V-row cell: its unit quad in the slot's plain V area)
-    const unsigned o_prod = cn < 16 ? (unsigned)((((w >> 2) * 4 + (cul >> 2)) * 64 + 16 * (w & 3) + cn) * 16)
-                                    : (unsigned)((WS_MAIN + (cn - 16) * kPH + 16 * w + cul) * 4);
+    const unsigned o_prod = (unsigned)((((w >> 2) * 4 + (cul >> 2)) * 64 + 16 * (w & 3) + cn) * 16);
     // publish the cell's value of step s: slot s & 1, and the sentinel into slot (s + 1) & 1
     auto pub = [&](int hb, float val, unsigned s) {
         // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]: quad lane 0 receives lanes 1, 2, 3
@@ -297,7 +265,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     // per-step operands of the cell (L2-resident: the per-frame tables and the ring), loaded
     // right after the hop E poll:
     //   pc[0..2] GRU2 cond (W_ih2[:, 512:] a2 + b_ih2), pc[3] fc1 cond, pc[4] fc2 cond (frame t)
-    // and right after the hop C poll (live only from fc3 to GRU1: registers are at the limit):
+    // and right after the hop C poll (live only from fc3 to GRU1: fewer registers held over the
+    // step's products):
     //   pg       Gumbel noise of (row, class cu) at step t        (ring slot t & 3)
     //   pp       P1(t + 1) of (row, unit cu), consumed by GRU1     (ring slot (t + 1) & 3)
     //   pv       v = W_ih1 w0 (r, z, n) and w0 of unit cu         (constants, L1-resident)
@@ -321,9 +290,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         int uu = cu;
         asm volatile("" : "+v"(uu));
         const unsigned cell_i = (unsigned)(cn * kPH + (uu & (kPH - 1)));
-        pg = bld(rr, (unsigned)WR_G * 4u + ((unsigned)(t & 3) * (unsigned)(kWRows * kPH) + cell_i) * 4u, 0);
+        pg = bld(rr, (unsigned)WR_G * 4u + ((unsigned)(t & 3) * 16u * kPH + cell_i) * 4u, 0);
         pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rr, ((unsigned)((t + 1) & 3) * (unsigned)(kWRows * kPH) + cell_i) * 16u, 0, 0));
+                                            rr, ((unsigned)((t + 1) & 3) * 16u * kPH + cell_i) * 16u, 0, 0));
         pv.x = bld(vr, (unsigned)uu * 4u, 0);
         pv.y = bld(vr, (unsigned)uu * 4u, kPH * 4);
         pv.z = bld(vr, (unsigned)uu * 4u, 2 * kPH * 4);
@@ -342,7 +311,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         int uu = u;
         asm volatile("" : "+v"(uu));
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
-        const unsigned cell_i = (unsigned)((tau & 3) * kWRows * kPH + n * kPH + uu);
+        const unsigned cell_i = (unsigned)((tau & 3) * 16 * kPH + n * kPH + uu);
         {
             // the noise of class u (a padding class beyond n_classes is drawn and never used)
             const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
@@ -386,76 +355,23 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rr, cell_i * 16u, 0, 0);
     };
-    // ring entries of step tau by the waves without cells: cell i = tid - 256 (waves 4-7); XV:
-    // waves 5-7, cells i = tid - 320 and i + 192
-    auto ring_step = [&](int tau) {
-        if constexpr (XV) {
-            const int i = tid - 320;
-            if (i >= 0 && i < 16 * R) ring_make(i >> 4, 16 * w + (i & 15), tau);
-            if (i >= 0 && i + 192 < 16 * R) ring_make((i + 192) >> 4, 16 * w + ((i + 192) & 15), tau);
-        } else {
-            const int i = tid - 256;
-            if (i >= 0 && i < 16 * R) ring_make(i >> 4, 16 * w + (i & 15), tau);
-        }
-    };
+    const bool lo = v < 4;  // waves 0-3 hold the epilogue cells
     __syncthreads();  // RowInfo in LDS
     // ring prologue: steps t0, t0 + 1, t0 + 2 (the loop forms t + 3 at step t). Drained before
     // the barrier: the first reads come right after it.
-    if (!cw) {
-        for (int k = 0; k < 3; ++k) ring_step(a.t0 + k);
+    if (!lo && tid - 256 < 16 * R) {
+        const int i = tid - 256;
+        for (int k = 0; k < 3; ++k) ring_make(i >> 4, 16 * w + (i & 15), a.t0 + k);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    // XV: the wave's V-row operand staging, (row 16, row 17) pairs per k of its K range
-    // (xs[k'][n'] at stg + 2 k' + n', k' < 64), in a partial tile of its own that is free when
-    // the stage's operands arrive (see each stage); v_stage writes the polled packets there
-    auto v_stage = [&](int stg, const u4v& cv) {
-        if (XV && l < 32) {
-            float* d = lds + stg + 8 * (l & 15) + (l >> 4);
-            d[0] = __uint_as_float(cv.x);
-            d[2] = __uint_as_float(cv.y);
-            d[4] = __uint_as_float(cv.z);
-            d[6] = __uint_as_float(cv.w);
-        }
-    };
-    // the staged pairs of k-steps 4q .. 4q + 3 of this lane's k-slot: {x16, x17} of k-step 4q + i
-    // is (i even ? p0 : p1) .xy / .zw
-    auto v_ops = [&](int stg, int q, float4& p0, float4& p1) {
-        const float* s = lds + stg + 32 * (l >> 4) + 8 * q;
-        p0 = *reinterpret_cast<const float4*>(s);
-        p1 = *reinterpret_cast<const float4*>(s + 4);
-    };
-    // {x16, x17} of k-step ks of this lane's k-slot
-    auto v_op = [&](int stg, int ks) -> v2f {
-        return *reinterpret_cast<const v2f*>(lds + stg + 32 * (l >> 4) + 2 * ks);
-    };
-    auto v_pair = [](const float4& p0, const float4& p1, int i) -> v2f {
-        return i == 0 ? (v2f){p0.x, p0.y} : i == 1 ? (v2f){p0.z, p0.w} : i == 2 ? (v2f){p1.x, p1.y} : (v2f){p1.z, p1.w};
-    };
-    // (two scalar v_fma_f32, not one v_pk_fma_f32: a packed operand wants the weight in an
-    // aligned register pair, which cost the weight file copies -- spills)
-    auto v_fma = [](float wgt, v2f x, v2f acc) { return (v2f){fmaf(wgt, x.x, acc.x), fmaf(wgt, x.y, acc.y)}; };
-    // sum over the 4 k-slots; lanes < 16 (k-slot 0, unit l) store rows 16, 17 of tile `base`
-    auto v_store = [&](v2f s, int base) {
-        s.x += __shfl_xor(s.x, 16);
-        s.y += __shfl_xor(s.y, 16);
-        s.x += __shfl_xor(s.x, 32);
-        s.y += __shfl_xor(s.y, 32);
-        if (l < 16) {
-            lds[base + 16 * 16 + wsw(16, l)] = s.x;
-            lds[base + 17 * 16 + wsw(17, l)] = s.y;
-        }
-    };
-    const int stg_s = WL_PS + v * NRW * 16;           // this wave's 1-tile partials
-    const int stg_a = WL_PA + v * 3 * NRW * 16;       // ... 3-tile partials (PA)
-    const int stg_h = WL_PH + v * 3 * NRW * 16;       // ... W_hh1 partials (PH)
-    u4v cv;
     // initial hop E: x1, h1 of step t0 (k_persist_init) as step t0 + 1 (canonicalised: a
     // signalling NaN in a carried state must not read as the sentinel)
     pub(WB_X1, __builtin_canonicalizef(x1c), (unsigned)a.t0 + 1u);
     pub(WB_H1, __builtin_canonicalizef(h1r), (unsigned)a.t0 + 1u);
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
+        t_now = t;
         const unsigned seq = (unsigned)t + 1u;
         const unsigned slot = (seq & 1u) * (unsigned)WSLOT * 4u;
         const unsigned so_x1 = (unsigned)(WB_X1 * WV) * 4u + slot, so_h1 = (unsigned)(WB_H1 * WV) * 4u + slot;
@@ -463,120 +379,29 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u + slot, so_y2 = (unsigned)(WB_Y2 * WV) * 4u + slot;
         u4v cc[4];
         bool fail = false;
-        // Products of a stage: MFMA tiles for rows 0-15 (B operands cc), and in the XV
-        // instance the V rows from the wave's staged pairs at `stg` (interleaved per k-quad, so
-        // the v_pk_fma_f32 issue in the MFMAs' shadow).
-        // Gates [G0, G1) of a 3-gate product into the tiles at `dst` (PA / PH layout): register
-        // tiles T0 + j (LDS = false) or the W_hh2 tiles in LDS (LDS = true). XV: the V operands
-        // at `stg` must not lie in a tile this call writes before its last gate's reads (the
-        // 3-gate products stage them in their gate-n tile, stage A in PS)
-        auto mmg = [&](auto t0c, auto g0c, auto g1c, auto ldsc, int dst, int stg) {
-            constexpr int T0 = decltype(t0c)::value, G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
-            constexpr bool LDSW = decltype(ldsc)::value;
-            if constexpr (XV) {
-                // gate by gate: one MFMA and one V accumulator live at a time (registers)
-#pragma unroll
-                for (int j = G0; j < G1; ++j) {
-                    v4f acc = {0.f, 0.f, 0.f, 0.f};
-                    v2f av = {0.f, 0.f};
-                    // the V operand of k-step ks + 1 is read while the MFMA of ks issues
-                    v2f xn = v_op(stg, 0);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        float4 aw = make_float4(0.f, 0.f, 0.f, 0.f);
-                        if constexpr (LDSW) {
-                            __builtin_amdgcn_sched_barrier(0);
-                            aw = hh2[((j * 8 + v) * 4 + q) * 64 + l];
-                        }
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int ks = 4 * q + k;
-                            if constexpr (!LDSW) __builtin_amdgcn_sched_barrier(0);  // one k-step of V operands live at a time
-                            const float wgt = LDSW ? f4c(aw, k) : WR(T0 + j, ks);
-                            const v2f x = xn;
-                            if (ks < 15) xn = v_op(stg, ks + 1);
-                            acc = mfma4(wgt, bop(cc, ks), acc);
-                            av = v_fma(wgt, x, av);
-                        }
-                    }
-                    *reinterpret_cast<v4f*>(lds + dst + ((v * 3 + j) * NRW + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc;
-                    v_store(av, dst + (v * 3 + j) * NRW * 16);
-                }
-            } else {
-                v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    float4 aw[3];
-                    if constexpr (LDSW) {
-                        __builtin_amdgcn_sched_barrier(0);  // one k-quad of LDS weights live at a time
-#pragma unroll
-                        for (int j = G0; j < G1; ++j) aw[j] = hh2[((j * 8 + v) * 4 + q) * 64 + l];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int ks = 4 * q + k;
-                        const float b = bop(cc, ks);
-#pragma unroll
-                        for (int j = G0; j < G1; ++j) acc[j] = mfma4(LDSW ? f4c(aw[j], k) : WR(T0 + j, ks), b, acc[j]);
-                    }
-                }
-#pragma unroll
-                for (int j = G0; j < G1; ++j)
-                    *reinterpret_cast<v4f*>(lds + dst + ((v * 3 + j) * NRW + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
-            }
-        };
-        using I0 = std::integral_constant<int, 0>;
-        using I1 [[maybe_unused]] = std::integral_constant<int, 1>;
-        using I2 [[maybe_unused]] = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        using REG = std::false_type;
-        using LDSW = std::true_type;
-        // 1-tile product with register tile T into the 1-tile partials (PS). The V operands are
-        // staged only after the first 8 MFMAs: PS[v] may still be read by an epilogue of this
-        // workgroup when the stage's operands of OTHER slots are already there (fc2, fc3); the
-        // MFMA partials themselves are written later still, as before.
-        auto mm1 = [&](auto tc) {
-            constexpr int T = decltype(tc)::value;
-            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-            v2f av0 = {0.f, 0.f}, av1 = {0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < 8; ks += 2) {
-                acc0 = mfma4(WR(T, ks), bop(cc, ks), acc0);
-                acc1 = mfma4(WR(T, ks + 1), bop(cc, ks + 1), acc1);
-            }
-            v_stage(stg_s, cv);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (XV) __builtin_amdgcn_sched_barrier(0);
-                float4 p0, p1;
-                if (XV) v_ops(stg_s, q, p0, p1);
-                acc0 = mfma4(WR(T, 8 + 2 * q), bop(cc, 8 + 2 * q), acc0);
-                acc1 = mfma4(WR(T, 9 + 2 * q), bop(cc, 9 + 2 * q), acc1);
-                if (XV) {
-                    av0 = v_fma(WR(T, 4 * q), v_pair(p0, p1, 0), av0);
-                    av1 = v_fma(WR(T, 4 * q + 1), v_pair(p0, p1, 1), av1);
-                    av0 = v_fma(WR(T, 4 * q + 2), v_pair(p0, p1, 2), av0);
-                    av1 = v_fma(WR(T, 4 * q + 3), v_pair(p0, p1, 3), av1);
-                }
-            }
-            *reinterpret_cast<v4f*>(lds + WL_PS + (v * NRW + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
-            if (XV) v_store(av0 + av1, WL_PS + v * NRW * 16);
-        };
         WSTAMP(0);
         // ================= hop E -> stage A: W_ih2[:, :512] x1 (critical) ==================
-        // (V operands staged in PS[v]: its last reader, the fc3 epilogue of the step before,
-        // ran before this workgroup's candidates went out, which every x1 waits for)
-        fail |= !w_poll<XV>(xr, o_cons, so_x1, bvalid, cc, vvalid, cv, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_x1, bvalid, cc, a.ctl, wh(1));
         prefetch(t);
-        v_stage(stg_s, cv);
         WSTAMP(1);
-        mmg(I0(), I0(), I3(), REG(), WL_PA, stg_s);
+        {
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const float b = bop(cc, ks);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(j, ks), b, acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
+        }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(2);
         if (lds[WL_FAIL] != 0.f) return;
-        // ================= GRU2 epilogue (cell waves) -> publish x2, h2 ====================
-        if (cw) {
+        // ================= GRU2 epilogue (waves 0-3) -> publish x2, h2 =====================
+        if (lo) {
             float x2 = 0.f;
             if (cell) {
                 float gi[3];
@@ -584,7 +409,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 for (int j = 0; j < 3; ++j) {
                     float s = 0.f;
 #pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * NRW + cn) * 16 + wsw(cn, cul)];
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + cn) * 16 + wsw(cn, cul)];
                     gi[j] = p_add(s, pc[j]);
                 }
                 h2r = p_gru(gi[0], gi[1], gi[2], g2r, g2z, g2n, h2r);
@@ -595,101 +420,118 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WSTAMP(3);
         // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
-        // SPLIT: the six off-path gate products (W_hh1 h1, W_hh2 h2 of the next step: 16 MFMAs a
-        // wave each) go two per exchange window -- W_hh1 r, z in hop A, W_hh1 n + W_hh2 r in hop B,
-        // W_hh2 z, n in hop C -- instead of three in hop A, three in hop B and none in hop C:
-        // 96 MFMAs per SIMD (1.28 us) overran a ~0.8 us hop. The V operands of a split product are
-        // staged in the gate-n tile of its partials, written only by that product's last gate.
-        // (V operands in PH[v]: read last by the gh sums before the stage-A barrier)
         {
-            fail |= !w_poll<XV>(xr, o_cons, so_h1, bvalid, cc, vvalid, cv, a.ctl);
-#if WRNN_WIDE_SPLIT
-            v_stage(stg_h + 2 * NRW * 16, cv);
+            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl, wh(2));
             WXSTAMP(26);
-            mmg(I3(), I0(), I2(), REG(), WL_PH, stg_h + 2 * NRW * 16);
-#else
-            v_stage(stg_h + 2 * NRW * 16, cv);  // (gate n's tile: written last, after all three reads)
-            WXSTAMP(26);
-            mmg(I3(), I0(), I3(), REG(), WL_PH, stg_h + 2 * NRW * 16);
-#endif
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const float b = bop(cc, ks);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(3 + j, ks), b, acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PH + ((v * 3 + j) * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
         }
         WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
-        fail |= !w_poll<XV>(xr, o_cons, so_x2, bvalid, cc, vvalid, cv, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3));
         WSTAMP(4);
-        mm1(std::integral_constant<int, 6>());
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(6, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(6, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
+        }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(5);
         if (lds[WL_FAIL] != 0.f) return;
-        // fc1 epilogue (cell waves): y1 = relu(fc1 x2 + fc1[:, 512:] a3 + b) -> publish
-        if (cw) {
+        // fc1 epilogue (waves 0-3): y1 = relu(fc1 x2 + fc1[:, 512:] a3 + b) -> publish
+        if (lo) {
             float y = 0.f;
             if (cell) {
                 float s = 0.f;
 #pragma unroll
-                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * NRW + cn) * 16 + wsw(cn, cul)];
+                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
                 y = p_add(s, pc[3]);
                 y = y > 0.f ? y : 0.f;
             }
             pub(WB_Y1, y, seq);
         }
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
-        // (V operands in PA[v]: read last by the GRU2 epilogue before the stage-B barrier)
         {
             WXSTAMP(28);
-#if WRNN_WIDE_SPLIT
-            // W_hh1 n (h1 again: its slot is rewritten only at step t + 2's hop E; the V operands
-            // are still staged in PH[v]'s gate-n tile since hop A)
-            fail |= !w_poll<XV>(xr, o_cons, so_h1, bvalid, cc, false, cv, a.ctl);
-            mmg(I3(), I2(), I3(), REG(), WL_PH, stg_h + 2 * NRW * 16);
-            fail |= !w_poll<XV>(xr, o_cons, so_h2, bvalid, cc, vvalid, cv, a.ctl);
-            v_stage(stg_a + 2 * NRW * 16, cv);
+            fail |= !w_poll(xr, o_cons, so_h2, bvalid, cc, a.ctl, wh(5));
             WXSTAMP(29);
-            mmg(I0(), I0(), I1(), LDSW(), WL_PA, stg_a + 2 * NRW * 16);
-#else
-            fail |= !w_poll<XV>(xr, o_cons, so_h2, bvalid, cc, vvalid, cv, a.ctl);
-            v_stage(stg_a + 2 * NRW * 16, cv);
-            WXSTAMP(29);
-            mmg(I0(), I0(), I3(), LDSW(), WL_PA, stg_a + 2 * NRW * 16);
-#endif
+            v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);  // one k-quad of LDS weights live at a time
+                float4 aw[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) aw[j] = hh2[((j * 8 + v) * 4 + q) * 64 + l];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float b = bop(cc, 4 * q + k);
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) acc[j] = mfma4(f4c(aw[j], k), b, acc[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
         }
         WXSTAMP(30);
         // ================= hop B -> stage C: fc2 y1 (critical) =============================
-        fail |= !w_poll<XV>(xr, o_cons, so_y1, bvalid, cc, vvalid, cv, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_y1, bvalid, cc, a.ctl, wh(6));
         WSTAMP(6);
-        mm1(std::integral_constant<int, 7>());
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(7, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(7, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
+        }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(7);
         if (lds[WL_FAIL] != 0.f) return;
-        if (cw) {  // fc2 epilogue: y2 = relu(fc2 y1 + fc2[:, 512:] a4 + b) -> publish
+        if (lo) {  // fc2 epilogue: y2 = relu(fc2 y1 + fc2[:, 512:] a4 + b) -> publish
             float y = 0.f;
             if (cell) {
                 float s = 0.f;
 #pragma unroll
-                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * NRW + cn) * 16 + wsw(cn, cul)];
+                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
                 y = p_add(s, pc[4]);
                 y = y > 0.f ? y : 0.f;
             }
             pub(WB_Y2, y, seq);
         }
-#if WRNN_WIDE_SPLIT
-        // ================= W_hh2 z, n (off-path, hop C wait; h2 again, V operands still
-        // staged in PA[v]'s gate-n tile since hop B) ======================================
-        fail |= !w_poll<XV>(xr, o_cons, so_h2, bvalid, cc, false, cv, a.ctl);
-        mmg(I0(), I1(), I3(), LDSW(), WL_PA, stg_a + 2 * NRW * 16);
-#endif
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
-        fail |= !w_poll<XV>(xr, o_cons, so_y2, bvalid, cc, vvalid, cv, a.ctl);
+        fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl, wh(8));
         prefetch_d(t);
         WSTAMP(8);
-        mm1(std::integral_constant<int, 8>());
+        {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(WR(8, ks), bop(cc, ks), acc0);
+                acc1 = mfma4(WR(8, ks + 1), bop(cc, ks + 1), acc1);
+            }
+            *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
+        }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(9);
         if (lds[WL_FAIL] != 0.f) return;
-        if (cw) {
+        if (lo) {
             const unsigned tag_hi = (seq & kTagSeqMask) << 11;
             // fc3 epilogue: candidate argmax_k (l_k + g_k) over the slot's 16 classes per row
             // (row cn = one DPP row of 16 lanes), published tagged by lane cul == 0
@@ -699,7 +541,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 if (cell && cu < a.n_classes) {
                     float s = 0.f;
 #pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * NRW + cn) * 16 + wsw(cn, cul)];
+                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
                     const float lg = p_add(s, lds[WL_BIAS + 96 + cul]);
                     p_dbg_logit<DBG>(a.dbg, t, crow, cu, a.B, a.n_classes, lg);
                     val = p_add(lg, pg);
@@ -720,7 +562,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     float s = 0.f;
 #pragma unroll
                     for (int vv = 0; vv < 8; ++vv)
-                        s += lds[(j < 3 ? WL_PH : WL_PA) + ((vv * 3 + j % 3) * NRW + cn) * 16 + wsw(cn, cul)];
+                        s += lds[(j < 3 ? WL_PH : WL_PA) + ((vv * 3 + j % 3) * 16 + cn) * 16 + wsw(cn, cul)];
                     gs[j] = p_add(s, lds[WL_BIAS + 16 * j + cul]);
                 }
                 g1r = gs[0];
@@ -747,6 +589,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     }
                     if (__all((q.y >> 11) == want && (q.w >> 11) == want)) break;
                     if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
+                        if (l == 0 && !ld_sc1_u(a.ctl + PC_ERR)) atomicCAS(a.ctl + PC_WHERE, 0u, wh(9) | ((unsigned)v << 19));
                         if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
                         fail = true;
                         break;
@@ -788,11 +631,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
         } else {
-            // waves without cells: ring entries of step t + 3 (written three steps ahead: their
-            // stores are drained by this wave's next poll, before the next stage-A barrier, and
-            // the cell waves read them two steps later; slot (t + 3) & 3 last held step t - 1,
-            // whose reads ended in step t - 1)
-            ring_step(t + 3);
+            // waves 4-7: ring entry of step t + 3 for cell i = tid - 256 (written three steps
+            // ahead: its stores are drained by this wave's next poll, before the next stage-A
+            // barrier, and waves 0-3 read it two steps later; slot (t + 3) & 3 last held step
+            // t - 1, whose reads ended in step t - 1)
+            const int i = tid - 256;
+            if (i < 16 * R) ring_make(i >> 4, 16 * w + (i & 15), t + 3);
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
@@ -825,11 +669,9 @@ size_t persist_wide_ring_floats() { return (size_t)kPG * WR_GROUP; }
 size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
 size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
 
-// scratch bytes of the production instance that runs nr rows per group (-1: unknown)
-int persist_wide_scratch(int nr) {
+int persist_wide_scratch() {
     hipFuncAttributes fa;
-    const void* fn = nr > 16 ? (const void*)k_persist_wide<false, true> : (const void*)k_persist_wide<false, false>;
-    if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
@@ -837,12 +679,8 @@ hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > kPM * 16 ||
         a.mode != 0 || a.wwide == nullptr || a.wring == nullptr)
         return hipErrorInvalidValue;
-    if (a.nr > 16) {
-        if (a.dbg.out) return persist_launch<k_persist_wide<true, true>>(persist_wide_lds_bytes(), a, s);
-        return persist_launch<k_persist_wide<false, true>>(persist_wide_lds_bytes(), a, s);
-    }
-    if (a.dbg.out) return persist_launch<k_persist_wide<true, false>>(persist_wide_lds_bytes(), a, s);
-    return persist_launch<k_persist_wide<false, false>>(persist_wide_lds_bytes(), a, s);
+    if (a.dbg.out) return persist_launch<k_persist_wide<true>>(persist_wide_lds_bytes(), a, s);
+    return persist_launch<k_persist_wide<false>>(persist_wide_lds_bytes(), a, s);
 }
 
 }  // namespace wrnn

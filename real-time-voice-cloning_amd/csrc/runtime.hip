@@ -2026,7 +2026,18 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         static const char* what[] = {"", "workgroups did not become co-resident",
                                      "exchange timeout", "workgroups not spread 32 per XCD",
                                      "aborted"};
-        fail(WRNN_ERR_HIP, std::string("persistent launch: ") + (err < 5 ? what[err] : "unknown error"));
+        unsigned wh[5] = {0, 0, 0, 0, 0};
+        (void)hipMemcpy(wh, (unsigned*)P.ctl.p + PC_WHERE, sizeof(wh), hipMemcpyDeviceToHost);
+        const unsigned where = wh[0];
+        if (where && std::getenv("WRNN_DEBUG_WHERE"))
+            std::fprintf(stderr, "[wrnn] timeout detail: mfma packets missing %u, V lane %u, V packet %08x .. %08x\n",
+                         wh[1], wh[2], wh[3], wh[4]);
+        std::string msg = std::string("persistent launch: ") + (err < 5 ? what[err] : "unknown error");
+        if (where)  // kernels_persist_wide.hip: the first timeout's site (PC_WHERE)
+            msg += " (site " + std::to_string(where >> 28) + ((where >> 27) & 1 ? " V packet" : "") +
+                   ", slot " + std::to_string((where >> 22) & 31) + ", wave " + std::to_string((where >> 19) & 7) +
+                   ", step " + std::to_string(where & 0x7ffff) + ")";
+        fail(WRNN_ERR_HIP, msg);
         return kPersistFallback;
     }
     if (a.phase_t >= 0) persist_phase_report(h, a.phase_t);
@@ -2170,16 +2181,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
             if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
             // (a variant with register spills is not used unless WRNN_WIDE_ALLOW_SCRATCH=1: A/B)
-            const bool any_scratch_ok = std::getenv("WRNN_WIDE_ALLOW_SCRATCH") != nullptr;
-            if (wmode && h->pw.wwide) {
+            const bool scratch_ok = persist_wide_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
+            if (wmode && h->pw.wwide && scratch_ok) {
                 if (wmode == 1) opts.clear();
-                // measured per step: 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows per
-                // group (the MFMA tiles cost the same for any row count; the exchanges and
-                // epilogues grow a little with the rows), fit 11.45 + 0.057 r; 17-18 rows (the
-                // XV instance: two rows on the VALU beside the tiles) 12.6
-                for (int r = 1; r <= kPWideRows; ++r)
-                    if (persist_wide_scratch(r) == 0 || any_scratch_ok)
-                        opts.push_back({r, true, r > 16 ? 12.6 : 11.45 + 0.057 * r});
+                // measured per step: round 2 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows
+                // per group (the MFMA tiles cost the same for any row count; the exchanges and
+                // epilogues grow a little with the rows); round 3 11.38 at 16 -- fit 10.5 + 0.055 r
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 10.5 + 0.055 * r});
             }
         } else {
             // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us

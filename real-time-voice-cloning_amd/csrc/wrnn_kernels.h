@@ -181,7 +181,9 @@ constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
 
 // control words (zeroed by the host before every launch); PC_ERR: 1 registration timeout,
 // 2 exchange timeout, 3 workgroups not spread 32 per XCD
-enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WORDS = 16 };
+// PC_WHERE: the first exchange timeout's site (wide kernel: site << 28 | V-packet bit << 27 |
+// slot << 22 | wave << 19 | step), reported in the error message
+enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WHERE = 10, PC_WORDS = 16 };
 // progress cadence of the reference's callback (fatchord_version.py:234: i % 100 == 0)
 constexpr int kProgressEvery = 100;
 // host-mapped abort request word, kAbortWord words past the progress word (a cache line of its
@@ -243,7 +245,7 @@ struct PersistArgs {
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 // Wide-row fatchord launch: up to kPWideRows rows per XCD group (8 kPWideRows per launch),
 // fp32 MFMA products, RAW categorical with <= 512 classes.
-constexpr int kPWideRows = 18;  // 16 MFMA columns + 2 VALU rows (kernels_persist_wide.hip XV)
+constexpr int kPWideRows = 16;
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
 size_t persist_wide_lds_bytes();
 size_t persist_wide_xbuf_floats();
@@ -251,7 +253,7 @@ hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s);
 size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
-int persist_wide_scratch(int nr);
+int persist_wide_scratch();
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
 // ---------------------------------------------------------------------------------------

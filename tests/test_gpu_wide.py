@@ -1,8 +1,7 @@
-"""The wide-row persistent launch (kernels_persist_wide.hip: up to 18 rows per XCD group -- 16
-on fp32 MFMA tiles, rows 16 and 17 on the VALU beside them -- distributed GRU1, five hops per
-step) against the reference's golden outputs and the oracle. ``WRNN_PERSIST_WIDE=1`` makes every
-launch of a call wide (1..18 rows per group); the default plan mixes wide and register-resident
-launches by cost (C4: one wide launch of 144 rows).
+"""The wide-row persistent launch (kernels_persist_wide.hip: 16 rows per XCD group, fp32 MFMA
+products, distributed GRU1, five hops per step) against the reference's golden outputs and the
+oracle. ``WRNN_PERSIST_WIDE=1`` makes every launch of a call wide (1..16 rows per group);
+the default plan mixes wide and register-resident launches by cost (C4: 128 + 16 rows).
 
 Reference step: vocoder/models/fatchord_version.py:192-236; bar: bit-exact 9-bit labels.
 """
@@ -51,8 +50,8 @@ def test_wide_golden_bit_exact(name, wide_only):
 
 @pytest.mark.parametrize('n_utts', [3, 13, 26])
 def test_wide_row_counts_match_oracle(n_utts, wide_only):
-    """5 fold rows per utterance -> 15 / 65 / 130 rows: 2, 9 and 17 rows per group (the last
-    with one VALU row: fold rows 128, 129 are in utterance 25), every row against the oracle."""
+    """5 fold rows per utterance -> 15 / 65 / 130 rows: 2, 9 and 16 + 1 rows per group (the
+    last over two wide launches), every row against the oracle."""
     import torch
     from oracle.wavernn_oracle import oracle_infer_waveform
     from test_gpu_parity import make_model
@@ -78,7 +77,7 @@ def test_wide_row_counts_match_oracle(n_utts, wide_only):
 
 
 def test_default_plan_uses_wide_launch_for_c4_rows():
-    """144 rows (C4 per GPU) -> one wide launch of 18 rows per group (round 2: 128 + 16)."""
+    """144 rows (C4 per GPU) -> one wide launch of 128 rows + one register-resident launch."""
     import torch
     from test_gpu_parity import make_model
     from wavernn_amd.hparams import sp
@@ -92,44 +91,3 @@ def test_default_plan_uses_wide_launch_for_c4_rows():
     assert roff[-1] == 144
     names = _stage_names(m)
     assert 'persist_wide' in names, names
-
-
-def test_valu_rows_labels_and_logits_match_oracle():
-    """The XV instance's VALU rows (group rows 16, 17 = fold rows 128..143 of an 18-rows-per-
-    group launch): 8 short utterances of 18 folds each (target 400, overlap 50) in one wide
-    launch; utterance 7 (fold rows 126..143: two MFMA rows, then the 16 VALU rows) against the
-    oracle on its noise stream -- every label, and the logits at four recorded steps within the
-    logit gate's 1e-5 (test_gpu_logits.py)."""
-    import torch
-    from oracle.wavernn_oracle import oracle_infer_waveform
-    from test_gpu_parity import make_model
-    from wavernn_amd.hparams import sp
-    from wavernn_amd.synth import synth_mel
-    meta, _ = golden_case('fatchord_raw9_tiny')
-    m, hp, sd = make_model(meta)
-    target, overlap, frames = 400, 50, 40
-    mels = [synth_mel(frames, 700 + u) / sp.max_abs_value for u in range(8)]
-    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
-    m.set_engine('persist')
-    m.set_seed(meta['noise_seed'])
-    m.enable_stage_timing(True)
-    B, S = m.fold_shape(frames, True, target, overlap)
-    steps = [0, 1, S // 2, S - 1]
-    m.set_debug_steps(steps)
-    lab, roff, S2 = m.generate_batch_device(dev, True, target, overlap)
-    assert B == 18 and S2 == S and roff[-1] == 144
-    assert m.plan_info() == [(0, 18, True)]
-    lab = lab.cpu().numpy()
-    u = 7
-    ref = oracle_infer_waveform(sd, hp, meta['model_type'], mels[u] * sp.max_abs_value,
-                                target=target, overlap=overlap, seed=meta['noise_seed'], stream=u,
-                                record_logits=steps)
-    got = lab[roff[u]:roff[u + 1]]
-    d = np.argwhere(got != ref['labels'])
-    assert len(d) == 0, f'first divergence {d[np.argmin(d[:, 1])]}'
-    rows = range(roff[u], roff[u + 1])
-    err = max(float(np.abs(m.debug_logits(s, rows).astype(np.float64) - ref['logits'][s]).max())
-              for s in steps)
-    print(f'VALU rows: max |dlogit| {err:.3g}')
-    assert err <= 1e-5
-    m.set_debug_steps([])
