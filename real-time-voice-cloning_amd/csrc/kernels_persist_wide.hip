@@ -105,9 +105,8 @@ __device__ __forceinline__ void wbar() {
 }
 
 // Poll this lane's 4 packets of one hop buffer slot (byte offset of packet 0: voff; packet p at
-// voff + 1 KiB p; so: the buffer and slot) until no value is the sentinel: all 4 in flight at
-// first (the data is often there already), then spin on packet 0 and reload the rest. Lanes
-// with valid == false (rows beyond the group's count) contribute zeros.
+// voff + 1 KiB p; so: the buffer and slot) until no value is the sentinel, all 4 in flight on
+// every pass. Lanes with valid == false (rows beyond the group's count) contribute zeros.
 // Why a sentinel is enough (no step tags): a producer writes step s into slot s & 1 and the
 // sentinel into slot (s + 1) & 1 (pub). Its next poll waits for every older vector memory
 // operation of the wave (vmcnt counts stores on gfx9), so that reset is in L2 before it
@@ -136,17 +135,21 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
         if (__all(ok)) return true;
     }
     while (true) {
-        if (valid) cc[0] = __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, kCpNT);
-        if (__all(!valid || p_ready(cc[0]))) {
+        // every packet reloaded per spin: a lane's 4 packets come from one producer slot's one
+        // store instruction, so when packet 0 lands the others have too and no second L2 round
+        // trip follows (round 3 A/B: 11.33 against 11.48 us per step spinning on packet 0,
+        // profiles/r03/ab_spin/)
+        if (valid) {
+            unsigned vo = voff;
+            asm volatile("" : "+v"(vo));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+        }
+        {
             bool ok = true;
             if (valid) {
-                unsigned vo = voff;
-                asm volatile("" : "+v"(vo));  // (offsets recomputed per use: hoisted ones pin registers)
 #pragma unroll
-                for (int i = 1; i < 4; ++i)
-                    cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
-#pragma unroll
-                for (int i = 1; i < 4; ++i) ok = ok && p_ready(cc[i]);
+                for (int i = 0; i < 4; ++i) ok = ok && p_ready(cc[i]);
             }
             if (__all(ok)) return true;
         }
