@@ -2026,12 +2026,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         static const char* what[] = {"", "workgroups did not become co-resident",
                                      "exchange timeout", "workgroups not spread 32 per XCD",
                                      "aborted"};
-        unsigned wh[5] = {0, 0, 0, 0, 0};
+        unsigned wh[2] = {0, 0};
         (void)hipMemcpy(wh, (unsigned*)P.ctl.p + PC_WHERE, sizeof(wh), hipMemcpyDeviceToHost);
         const unsigned where = wh[0];
         if (where && std::getenv("WRNN_DEBUG_WHERE"))
-            std::fprintf(stderr, "[wrnn] timeout detail: mfma packets missing %u, V lane %u, V packet %08x .. %08x\n",
-                         wh[1], wh[2], wh[3], wh[4]);
+            std::fprintf(stderr, "[wrnn] timeout detail: the timed-out poll's packets were %s\n",
+                         wh[1] ? "missing" : "all present (a later check failed)");
         std::string msg = std::string("persistent launch: ") + (err < 5 ? what[err] : "unknown error");
         if (where)  // kernels_persist_wide.hip: the first timeout's site (PC_WHERE)
             msg += " (site " + std::to_string(where >> 28) + ((where >> 27) & 1 ? " V packet" : "") +
