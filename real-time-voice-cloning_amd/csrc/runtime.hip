@@ -2034,7 +2034,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
                          wh[1] ? "missing" : "all present (a later check failed)");
         std::string msg = std::string("persistent launch: ") + (err < 5 ? what[err] : "unknown error");
         if (where)  // kernels_persist_wide.hip: the first timeout's site (PC_WHERE)
-            msg += " (site " + std::to_string(where >> 28) + ((where >> 27) & 1 ? " V packet" : "") +
+            msg += " (site " + std::to_string(where >> 28) +
                    ", slot " + std::to_string((where >> 22) & 31) + ", wave " + std::to_string((where >> 19) & 7) +
                    ", step " + std::to_string(where & 0x7ffff) + ")";
         fail(WRNN_ERR_HIP, msg);
