@@ -342,10 +342,9 @@ __device__ __forceinline__ float wave_sum_all(float v) {
     return ((lanef(v, 0) + lanef(v, 16)) + lanef(v, 32)) + lanef(v, 48);
 }
 __device__ __forceinline__ void amax_step(float& v, int& i, float v2, int i2) {
-    if (v2 > v || (v2 == v && i2 < i)) {
-        v = v2;
-        i = i2;
-    }
+    const bool take = (v2 > v) | ((v2 == v) & (i2 < i));  // bitwise: no exec-mask branches
+    v = take ? v2 : v;
+    i = take ? i2 : i;
 }
 template <int CTRL>
 __device__ __forceinline__ void amax_dpp(float& v, int& i) {

@@ -184,14 +184,19 @@ template <int CTRL>
 __device__ __forceinline__ int pdpp_i(int v) {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
 }
+// (v, k) <- (v2, k2) when v2 is larger, or equal with a lower class. Bitwise, not `||` / `&&`:
+// the short-circuit form compiled to exec-mask branches (~17 instructions per step on the
+// candidate publish and sample paths); this is compares + two v_cndmask
+__device__ __forceinline__ void amax_take(float& v, int& k, float v2, int k2) {
+    const bool take = (v2 > v) | ((v2 == v) & (k2 < k));
+    v = take ? v2 : v;
+    k = take ? k2 : k;
+}
 template <int CTRL>
 __device__ __forceinline__ void amax_dpp_step(float& v, int& k) {
     const float v2 = pdpp<CTRL>(v);
     const int k2 = pdpp_i<CTRL>(k);
-    if (v2 > v || (v2 == v && k2 < k)) {
-        v = v2;
-        k = k2;
-    }
+    amax_take(v, k, v2, k2);
 }
 // argmax over the 16 lanes of a DPP row (value, class); ties -> lowest class; all lanes get it
 __device__ __forceinline__ void row16_argmax(float& v, int& k) {
@@ -213,10 +218,7 @@ __device__ __forceinline__ void half_argmax(float& v, int& k) {
     row16_argmax(v, k);
     const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x142, 0xA, 0xF, false));
     const int k2 = __builtin_amdgcn_update_dpp(k, k, 0x142, 0xA, 0xF, false);
-    if (v2 > v || (v2 == v && k2 < k)) {
-        v = v2;
-        k = k2;
-    }
+    amax_take(v, k, v2, k2);
 }
 
 // Buffer-resource access: a uniform (SGPR) base and a 32-bit per-lane byte offset, so no
