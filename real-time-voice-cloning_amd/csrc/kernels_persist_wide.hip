@@ -96,7 +96,8 @@ __device__ __forceinline__ float bop(const u4v (&cc)[4], int ks) {
 __device__ __forceinline__ int wsw(int n, int o) { return ((((o >> 2) ^ (n >> 1)) & 3) << 2) | (o & 3); }
 
 __device__ __forceinline__ bool p_ready(const u4v& q) {
-    return q.x != kSent && q.y != kSent && q.z != kSent && q.w != kSent;
+    // bitwise: the short-circuit form compiled to a branch and a wait per packet
+    return (q.x != kSent) & (q.y != kSent) & (q.z != kSent) & (q.w != kSent);
 }
 
 // LDS-only workgroup barrier: no wait on outstanding global loads (prefetches stay in flight)
@@ -114,24 +115,28 @@ __device__ __forceinline__ void wbar() {
 // read such a later publication, so it sees the reset or the new value, never step s - 1. And
 // slot s & 1 is rewritten (step s + 2) only after every consumer has published past its reads
 // of step s.
+// The 4 packet loads of a poll round. Unconditional: a lane without an operand loads from an
+// out-of-range offset, which reads 0 ("ready"), so every path carries the same loads and the
+// compiler's waits stay counted (a branch around them made the waits after it conservative).
+// w_issue alone: the first round issued early, for an off-path operand published long before
+// its use, checked later by w_poll with pre = true.
+__device__ __forceinline__ void w_issue(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4]) {
+    unsigned vo = valid ? voff : 0x80000000u;
+    asm volatile("" : "+v"(vo));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+}
 // On a timeout the first poller records its site in PC_WHERE (`where`: site << 28 | slot << 22 |
 // step; the wave is added here) and whether its packets were missing, for the error message.
 __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4],
-                                       unsigned* ctl, unsigned where) {
+                                       unsigned* ctl, unsigned where, bool pre = false) {
     const unsigned t0 = p_now();
     unsigned nsp = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cc[i] = (u4v){0u, 0u, 0u, 0u};
+    if (!pre) w_issue(xr, voff, so, valid, cc);
     {
         bool ok = true;
-        if (valid) {
-            unsigned vo = voff;
-            asm volatile("" : "+v"(vo));
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ok = ok && p_ready(cc[i]);
-        }
+        for (int i = 0; i < 4; ++i) ok &= p_ready(cc[i]);
         if (__all(ok)) return true;
     }
     while (true) {
@@ -139,25 +144,18 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
         // store instruction, so when packet 0 lands the others have too and no second L2 round
         // trip follows (round 3 A/B: 11.33 against 11.48 us per step spinning on packet 0,
         // profiles/r03/ab_spin/)
-        if (valid) {
-            unsigned vo = voff;
-            asm volatile("" : "+v"(vo));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
-        }
+        w_issue(xr, voff, so, valid, cc);
         {
             bool ok = true;
-            if (valid) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ok = ok && p_ready(cc[i]);
-            }
+            for (int i = 0; i < 4; ++i) ok &= p_ready(cc[i]);
             if (__all(ok)) return true;
         }
         if ((++nsp & 63) == 0 && (ld_sc1_u(ctl + PC_ERR) || p_now() - t0 > kSpinTicks)) {
             if (!ld_sc1_u(ctl + PC_ERR)) {  // the first to time out records where
                 bool mok = true;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) mok = mok && (!valid || p_ready(cc[i]));
+                for (int i = 0; i < 4; ++i) mok &= p_ready(cc[i]);
                 const bool mbad = !__all(mok);
                 if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | ((threadIdx.x >> 6) << 19)) == 0u)
                     ctl[PC_WHERE + 1] = mbad ? 1u : 0u;
@@ -251,6 +249,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     const unsigned o_cons = (unsigned)((v * 4 * 64 + l) * 16);
     const unsigned o_prod = (unsigned)((((w >> 2) * 4 + (cul >> 2)) * 64 + 16 * (w & 3) + cn) * 16);
     // publish the cell's value of step s: slot s & 1, and the sentinel into slot (s + 1) & 1
+    // every wave and lane issues the publish stores; a lane that does not publish stores to an
+    // out-of-range offset (dropped by the buffer range check), so every path through a stage
+    // carries the same stores and a poll issued before them need not wait for their acks
+    auto pub_if = [&](bool on, int hb, float val, unsigned s) {
+        const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
+        const unsigned vo = on && cell && (cul & 3) == 0 ? o_prod : 0x80000000u;
+        const unsigned sb = (unsigned)(hb * WV) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr, vo,
+            sb + (s & 1u) * (unsigned)WSLOT * 4u, 0);
+        __builtin_amdgcn_raw_buffer_store_b128((u4v){kSent, kSent, kSent, kSent}, xr, vo,
+                                               sb + ((s + 1u) & 1u) * (unsigned)WSLOT * 4u, 0);
+    };
     auto pub = [&](int hb, float val, unsigned s) {
         // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]: quad lane 0 receives lanes 1, 2, 3
         const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
@@ -382,6 +393,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u + slot, so_y2 = (unsigned)(WB_Y2 * WV) * 4u + slot;
         u4v cc[4];
         bool fail = false;
+        float x2s = 0.f;  // the value a lo wave publishes (x2, then y1)
         WSTAMP(0);
         // ================= hop E -> stage A: W_ih2[:, :512] x1 (critical) ==================
         fail |= !w_poll(xr, o_cons, so_x1, bvalid, cc, a.ctl, wh(1));
@@ -403,6 +415,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         wbar();
         WSTAMP(2);
         if (lds[WL_FAIL] != 0.f) return;
+        // h1 (published with x1, read above) loads now: in flight over the GRU2 epilogue, so the
+        // off-path W_hh1 h1 starts without an L2 round trip
+        w_issue(xr, o_cons, so_h1, bvalid, cc);
         // ================= GRU2 epilogue (waves 0-3) -> publish x2, h2 =====================
         if (lo) {
             float x2 = 0.f;
@@ -418,13 +433,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 h2r = p_gru(gi[0], gi[1], gi[2], g2r, g2z, g2n, h2r);
                 x2 = p_add(x1c, h2r);
             }
-            pub(WB_X2, x2, seq);
-            pub(WB_H2, h2r, seq);
+            x2s = x2;
         }
+        pub_if(lo, WB_X2, x2s, seq);
+        pub_if(lo, WB_H2, h2r, seq);
         WSTAMP(3);
         // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
         {
-            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl, wh(2));
+            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl, wh(2), true);
             WXSTAMP(26);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -440,6 +456,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
         fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3));
+        // h2 (published with x2, just read) loads now: in flight over fc1 and its epilogue
+        u4v ch[4];
+        w_issue(xr, o_cons, so_h2, bvalid, ch);
         WSTAMP(4);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -464,12 +483,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 y = p_add(s, pc[3]);
                 y = y > 0.f ? y : 0.f;
             }
-            pub(WB_Y1, y, seq);
+            x2s = y;
         }
+        pub_if(lo, WB_Y1, x2s, seq);
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
             WXSTAMP(28);
-            fail |= !w_poll(xr, o_cons, so_h2, bvalid, cc, a.ctl, wh(5));
+            fail |= !w_poll(xr, o_cons, so_h2, bvalid, ch, a.ctl, wh(5), true);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cc[i] = ch[i];
             WXSTAMP(29);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
