@@ -126,6 +126,13 @@ __device__ __forceinline__ void w_issue(rsrc_t xr, unsigned voff, unsigned so, b
 #pragma unroll
     for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
 }
+// Packet i of a poll round alone (see w_issue): issued into a packet register an off-path
+// product has finished reading, so a critical hop's first round needs no extra registers.
+__device__ __forceinline__ void w_issue1(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v& c, int i) {
+    unsigned vo = valid ? voff : 0x80000000u;
+    asm volatile("" : "+v"(vo));
+    c = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
+}
 // On a timeout the first poller records its site in PC_WHERE (`where`: site << 28 | slot << 22 |
 // step; the wave is added here) and whether its packets were missing, for the error message.
 __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4],
@@ -448,6 +455,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 const float b = bop(cc, ks);
 #pragma unroll
                 for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(3 + j, ks), b, acc[j]);
+                // x2's first poll round, packet by packet as the h1 packets are consumed (the
+                // same for y1 over W_hh2 h2 measured no gain: 125.2 against 125.5 ms per launch)
+                if ((ks & 3) == 3) w_issue1(xr, o_cons, so_x2, bvalid, cc[ks >> 2], ks >> 2);
             }
 #pragma unroll
             for (int j = 0; j < 3; ++j)
@@ -455,7 +465,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
-        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3));
+        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3), true);
         // h2 (published with x2, just read) loads now: in flight over fc1 and its epilogue
         u4v ch[4];
         w_issue(xr, o_cons, so_h2, bvalid, ch);
