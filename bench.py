@@ -14,8 +14,10 @@ N>1    : one process per GPU (torchrun); utterances are independent, so each ran
 Also reported: roofline of the dominant recurrent kernel (HIP events on its stream over the
 timed region; HBM, fp32 and latency-floor fractions), the CPU baseline (oracle restatement of
 the reference generate() on this host: the whole utterance on the default thread count, plus
-bounded 1-thread and all-core legs; rank 0, N=1 only) and `parity`: the timed call's labels and
-waveform against that same oracle run (same seed and noise stream).
+bounded 1-thread and all-core legs; rank 0 after the timed region -- at N>1 on an utterance of the
+last rank) and `parity`: the timed call's labels and waveform against that same oracle run (same
+seed and noise stream). `config.lib_build` names the timed HIP library (SHA-256 prefix);
+`roofline.traffic_lib_build` the library the PMC counters were read from.
 """
 import argparse
 import json
@@ -52,10 +54,25 @@ def parse():
 
 
 def _pmc_traffic(kernel, workload):
+    # WRNN_PMC_TRAFFIC: a table folded on the box from this build's own counter passes
+    # (tools/measure_r04.sh), so the line's counters come from the binary it times
+    path = os.environ.get('WRNN_PMC_TRAFFIC') or os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     try:
-        with open(os.path.join(REPO, 'profiles', 'pmc_traffic.json')) as f:
+        with open(path) as f:
             return json.load(f).get(f'{kernel}|{workload}')
     except (OSError, ValueError):
+        return None
+
+
+def lib_build_id():
+    """First 16 hex digits of the SHA-256 of the loaded HIP library: names the binary a bench
+    line (and a PMC pass, tools/pmc_traffic.py) measured."""
+    import hashlib
+    from wavernn_amd import _abi
+    try:
+        with open(_abi.LIB_PATH, 'rb') as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
         return None
 
 
@@ -180,11 +197,14 @@ def logit_gate(args, sd, hp, model, mel_dev, mel, gpu_rows, seed, stream):
     r = _oracle_run(args, sd, hp, mel, torch.get_num_threads(), seed=seed, stream=stream,
                     record_logits=set(steps), track_margin=model.categorical, post=False)
     ref = np.stack([r['logits'][t] for t in steps])
-    out = {'steps': steps, 'max_abs_logit_err': float(np.abs(got.astype(np.float64) - ref).max()),
+    err = float(np.abs(got.astype(np.float64) - ref).max())
+    out = {'steps': steps, 'max_abs_logit_err': err,
            'max_abs_logit': float(np.abs(ref).max()), 'tolerance': 1e-5,
            'rerun_identical': bool(np.array_equal(rerun, gpu_rows))}
     if 'margin' in r:
         out['min_top2_gap'] = r['margin']['min_gap']
+        # how many times the logit error fits into the closest decision of the call
+        out['gap_over_err'] = r['margin']['min_gap'] / err if err > 0 else None
         out['min_top2_gap_at'] = [r['margin']['step'], r['margin']['row']]
         out['min_top2_gap_over'] = f"{r['B']} rows x {r['S']} steps (log(p/q) top-1 - top-2)"
     return out
@@ -334,6 +354,11 @@ def main():
         # dominant kernel = largest avg duration x launches
         dom = max(info, key=lambda r: (r[3] if r[3] == r[3] else 0) * r[4])
         name, by, fl, us, n = dom
+        us_rank = us
+        if world > 1:  # the slowest rank's launch bounds the job: roofline on the max over ranks
+            t = torch.tensor([us], device='cpu' if rehearse else dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            us = float(t.item())
         achieved = by / (us * 1e-6) / 1e9 if us > 0 else None
         kernel = {'persist': 'k_persist', 'persist_wide': 'k_persist_wide'}.get(name, f'k_stage<{name}>')
         roof = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved,
@@ -341,6 +366,8 @@ def main():
                 'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': None,
                 'avg_us': us, 'launches_timed': n, 'alg_bytes_per_launch': by,
                 'flops_per_launch': fl,
+                'avg_us_over': ('max over ranks (all-reduced); rank 0: %.1f us' % us_rank
+                                if world > 1 else 'one rank'),
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
                 'fp32_frac': fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
@@ -365,6 +392,8 @@ def main():
         if pmc:
             roof['traffic'] = pmc['traffic_bytes']
             roof['traffic_source'] = pmc['source']
+            roof['traffic_lib_build'] = pmc.get('lib_build')
+            roof['traffic_from_benched_build'] = pmc.get('lib_build') == lib_build_id()
             roof['traffic_note'] = pmc['correction']
             # counter-backed utilisation of the same kernel (SQ pass, tools/pmc_traffic.py):
             # MFMA pipe busy fraction over all 1024 SIMDs, LDS bank-conflict share, wave states
@@ -387,7 +416,8 @@ def main():
                    'parallelism': (f'utterances sharded over {world} GPU(s); fold rows gathered '
                                    f'to rank 0 (RCCL gather), f64 post-processing on rank 0'
                                    if world > 1 else 'one GPU'),
-                   'engine': model.last_engine(), 'persist_fallbacks': fb[0]},
+                   'engine': model.last_engine(), 'persist_fallbacks': fb[0],
+                   'lib_build': lib_build_id()},
         'roofline': roof,
         'cpu_baseline': None,
     }
@@ -417,12 +447,14 @@ def main():
         result['parity']['logits'] = logit_gate(args, sd, hp, model, mels[0], mels_host[0],
                                                 gpu_rows, seed, stream)
     elif rank == 0 and world > 1 and args.cpu_seconds > 0:
-        # N > 1: one utterance of the LAST rank's shard, gathered over RCCL, against the oracle
-        # on its global stream (world-size invariance: the same labels as at N = 1)
+        # N > 1: the same CPU legs as N = 1, after the timed region and its barrier, on one
+        # utterance of the LAST rank's shard (gathered over RCCL): the whole-utterance oracle leg
+        # is also that utterance's parity check on its global stream (world-size invariance:
+        # the same labels as at N = 1)
         u = plan[world - 1][0]
         stream = last['base'] + u
-        result['parity'] = parity_check(args, sd, hp, mels_host[u], last['rows'][u], wavs[u],
-                                        seed, stream)
+        result['cpu_baseline'], result['parity'] = cpu_baseline(
+            args, sd, hp, mels_host[u], last['rows'][u], wavs[u], seed, stream)
         result['parity'].update(utterance=u, from_rank=world - 1)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -99,8 +99,15 @@ def _fan_in(name, shape):
     return int(np.prod(shape[1:]))
 
 
-def synth_state_dict(hp, model_type, seed=0, logit_scale=1.0, feat_dims=80):
-    """Deterministic float32 weights {name: ndarray} (plus ``step``) for a topology."""
+def synth_state_dict(hp, model_type, seed=0, logit_scale=1.0, feat_dims=80, gru_scale=1.0,
+                     fc_scale=1.0):
+    """Deterministic float32 weights {name: ndarray} (plus ``step``) for a topology.
+
+    ``logit_scale`` scales the output layer (fatchord/geneing fc3, runtimeracer fc5),
+    ``gru_scale`` every GRU parameter and ``fc_scale`` the hidden fc layers: the knobs that move
+    the seeded init towards a trained checkpoint's statistics (saturated gates, peaked posteriors;
+    tests/golden/gen_golden.py 'trained-like' fixtures). Scaling happens after the draws, so
+    the other tensors do not depend on the knobs."""
     rng = np.random.Generator(np.random.PCG64(seed))
     spec = state_dict_spec(hp, model_type, feat_dims)
     sd = {}
@@ -134,6 +141,11 @@ def synth_state_dict(hp, model_type, seed=0, logit_scale=1.0, feat_dims=80):
     if logit_scale != 1.0:
         sd[f'{last_fc}.weight'] = (sd[f'{last_fc}.weight'] * np.float32(logit_scale)).astype(np.float32)
         sd[f'{last_fc}.bias'] = (sd[f'{last_fc}.bias'] * np.float32(logit_scale)).astype(np.float32)
+    for name in list(sd):
+        scale = (gru_scale if name.startswith('rnn') else
+                 fc_scale if name.startswith('fc') and not name.startswith(last_fc + '.') else 1.0)
+        if scale != 1.0:
+            sd[name] = (sd[name] * np.float32(scale)).astype(np.float32)
     sd['step'] = np.zeros((1,), dtype=np.int64)
     return sd
 

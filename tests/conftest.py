@@ -18,13 +18,35 @@ def pytest_configure(config):
     config.addinivalue_line('markers', 'slow: long-running CPU test')
 
 
-def golden_meta():
+def golden_meta(regime='bit-exact'):
+    """Fixtures by parity regime: 'bit-exact' (every case whose labels a correct fp32
+    implementation must reproduce), 'divergence-onset' (the chaotic trained-like case, see
+    tests/golden/gen_golden.py), or None for all."""
     with open(os.path.join(GOLDEN, 'golden_meta.json')) as f:
-        return {k: v for k, v in json.load(f).items() if not k.startswith('_')}
+        return {k: v for k, v in json.load(f).items() if not k.startswith('_')
+                and (regime is None or v.get('regime', 'bit-exact') == regime)}
 
 
 def golden_case(name):
-    return golden_meta()[name], dict(np.load(os.path.join(GOLDEN, name + '.npz')))
+    return golden_meta(None)[name], dict(np.load(os.path.join(GOLDEN, name + '.npz')))
+
+
+def state_dict_of(meta):
+    """The fixture's seeded weights (synth_state_dict with the case's statistics knobs)."""
+    from wavernn_amd.synth import synth_state_dict
+    return synth_state_dict(hparams_of(meta), meta['model_type'], seed=meta['weight_seed'],
+                            logit_scale=meta['logit_scale'], gru_scale=meta.get('gru_scale', 1.0),
+                            fc_scale=meta.get('fc_scale', 1.0))
+
+
+def wave_equal(wav, gold):
+    """Bit equality with the reference's f64 waveform, stored whole or as its SHA-256 (the
+    full-size trained-like fixtures)."""
+    if 'wav' in gold:
+        return wav.shape == gold['wav'].shape and np.array_equal(wav, gold['wav'])
+    import hashlib
+    return (len(wav) == int(gold['wav_len']) and wav.dtype == np.float64 and
+            hashlib.sha256(np.ascontiguousarray(wav).tobytes()).digest() == gold['wav_sha256'].tobytes())
 
 
 def is_continuous(meta):

@@ -8,9 +8,11 @@ reference's (test_gpu_parity.py), its recurrence is teacher-forced by the refere
 history: the logits it records at those steps (wrnn_set_debug_steps / wrnn_debug_logits,
 written by the kernel that runs the call) are comparable element for element.
 
-Bar: max |logit_gpu - logit_ref| <= 1e-5 on every fixture, every engine and launch kind. The
-test also reports the smallest top-2 gap of the recorded steps' Gumbel-max decisions, i.e. how
-far each decision was from flipping, next to the error.
+Bar: max |logit_gpu - logit_ref| <= 1e-5 x max(1, max |logit_ref|) on every fixture, every engine
+and launch kind: 1e-5 absolute at the seeded-init scale (|logit| <= 0.2), relative for the
+trained-like fixtures (|logit| up to ~20, where one fp32 ulp is already 1.9e-6). The test also
+reports the smallest top-2 gap of the recorded steps' Gumbel-max decisions, i.e. how far each
+decision was from flipping, next to the error, and requires gap > 2 x error.
 """
 import os
 
@@ -25,7 +27,8 @@ LOGIT_ABS_TOL = 1e-5
 
 CASES = [(k, e) for k in golden_meta() for e in ('persist', 'chain')]
 # the wide MFMA launch (kernels_persist_wide.hip) on the fatchord RAW <= 512-class fixtures
-WIDE = ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny', 'fatchord_raw9_config1']
+WIDE = ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny', 'fatchord_raw9_config1',
+        'fatchord_raw9_c2_peaked']
 
 
 def _run(name, engine, wide=False, monkeypatch=None):
@@ -73,9 +76,10 @@ def _check(name, meta, gold, got):
     assert np.isfinite(got).all(), f'{name}: a recorded logit was never written'
     err = float(np.abs(got.astype(np.float64) - ref.astype(np.float64)).max())
     gap = _gap(meta, gold, got)
-    print(f'{name}: max |dlogit| {err:.3g} (|logit| <= {np.abs(ref).max():.3g}), '
-          f'min top-2 gap {gap}')
-    assert err <= LOGIT_ABS_TOL, f'{name}: max logit error {err}'
+    tol = LOGIT_ABS_TOL * max(1.0, float(np.abs(ref).max()))
+    print(f'{name}: max |dlogit| {err:.3g} (|logit| <= {np.abs(ref).max():.3g}, tol {tol:.3g}), '
+          f'min top-2 gap {gap}, gap / err {gap / err if gap and err else None}')
+    assert err <= tol, f'{name}: max logit error {err}'
     if gap is not None:
         assert gap > 2 * err  # every recorded decision is farther from a flip than the error
 

@@ -6,7 +6,7 @@ bit-exact (f64 post-processing is the reference's own numpy/scipy code); MOL and
 import numpy as np
 import pytest
 
-from conftest import golden_case, golden_meta, hparams_of, is_continuous
+from conftest import golden_case, golden_meta, hparams_of, is_continuous, state_dict_of, wave_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -16,10 +16,8 @@ MOL_RMS_TOL = 1e-4
 def make_model(meta):
     from wavernn_amd.model import WaveRNN
     from wavernn_amd.hparams import sp
-    from wavernn_amd.synth import synth_state_dict
     hp = hparams_of(meta)
-    sd = synth_state_dict(hp, meta['model_type'], seed=meta['weight_seed'],
-                          logit_scale=meta['logit_scale'])
+    sd = state_dict_of(meta)
     m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
                 hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
                 mode=hp.mode, model_type=meta['model_type'], device=0)
@@ -71,8 +69,7 @@ def test_raw_labels_and_wave_bit_exact(name, engine):
     agree = float((lab == gold['labels']).mean())
     assert agree == 1.0, f'{name}/{engine}: label agreement {agree}, first divergence (row, step) ' \
                          f'{first_divergence(lab, gold["labels"])}'
-    assert wav.dtype == np.float64 and wav.shape == gold['wav'].shape
-    assert np.array_equal(wav, gold['wav'])
+    assert wav.dtype == np.float64 and wave_equal(wav, gold)
 
 
 @pytest.mark.parametrize('name,engine', MOL_CASES)
@@ -133,9 +130,7 @@ def test_persist_p1_matches_oracle(case):
     from wavernn_amd.synth import synth_mel
     meta, gold, m, wav = run_case(case, engine='persist')
     hp = hparams_of(meta)
-    from wavernn_amd.synth import synth_state_dict
-    sd = synth_state_dict(hp, meta['model_type'], seed=meta['weight_seed'],
-                          logit_scale=meta['logit_scale'])
+    sd = state_dict_of(meta)
     o = OracleWaveRNN(sd, hp, meta['model_type'])
     T = meta['n_frames']
     mel = torch.from_numpy(synth_mel(T, meta['mel_seed'])[None] / sp.max_abs_value)

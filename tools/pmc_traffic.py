@@ -1,9 +1,12 @@
 """Fold rocprofv3 counter passes into profiles/pmc_traffic.json, which bench.py reads for
 roofline.traffic and the counter-backed fractions (rocprofv3 cannot run inside the bench process).
 
-usage: python tools/pmc_traffic.py <pass dir> <round dir> [bench args note]
+usage: python tools/pmc_traffic.py <pass dir> <round dir> [<table json>]
   <pass dir>: tools/pmc_r03.sh output (gpurun_out/pmc3): <w>_fetch/, <w>_write/, <w>_sq/ per
-              workload w (c2, c4, ...), each with run_counter_collection.csv
+              workload w (c2, c4, ...), each with run_counter_collection.csv, and lib_build
+              (the SHA-256 prefix of the library the passes ran, bench.lib_build_id)
+  <table json>: where to write the table (default profiles/pmc_traffic.json; the measurement
+              script folds on the box into gpurun_out/ and points the bench at it)
 Copies the CSVs to <round dir>/pmc/ and writes one entry per workload, keyed
 '<kernel>|<bench workload string>', with per-launch values of the dominant kernel:
   traffic_bytes   HBM bytes: FETCH_SIZE x 2 + WRITE_SIZE (KiB counters; MI355X_MICROARCH.md HBM
@@ -69,6 +72,11 @@ def main():
     os.makedirs(os.path.join(out, 'pmc'), exist_ok=True)
     jpath = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     table = json.load(open(jpath)) if os.path.exists(jpath) else {}
+    if len(sys.argv) > 3:
+        jpath = sys.argv[3]
+    lib_build = None
+    if os.path.exists(os.path.join(src, 'lib_build')):
+        lib_build = open(os.path.join(src, 'lib_build')).read().strip() or None
     for key, (extra, wl, kernel) in WORKLOADS.items():
         paths = {p: os.path.join(src, f'{key}_{p}', 'run_counter_collection.csv')
                  for p in ('fetch', 'write', 'sq')}
@@ -81,7 +89,7 @@ def main():
         write, _, _ = per_launch(paths['write'], kernel)
         traffic = (2 * fetch['FETCH_SIZE'] + write['WRITE_SIZE']) * 1024.0
         rel = os.path.relpath(os.path.join(out, 'pmc'), REPO)
-        e = {'kernel': kname, 'launches': n, 'fetch_size_kib': fetch['FETCH_SIZE'],
+        e = {'kernel': kname, 'launches': n, 'lib_build': lib_build, 'fetch_size_kib': fetch['FETCH_SIZE'],
              'write_size_kib': write['WRITE_SIZE'], 'traffic_bytes': traffic, 'correction': CORR,
              'source': f'{rel}/{key}_fetch.csv, {rel}/{key}_write.csv: rocprofv3 --pmc FETCH_SIZE | '
                        f'WRITE_SIZE (separate passes) --kernel-include-regex {kernel} -- python3 '
