@@ -222,6 +222,13 @@ int wrnn_post_assemble(const int16_t* labels, int nf, int S, int overlap, const 
 int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,
                     float beta, float* out);
 
+/* Host-side exhaustive check of the wide launch's exchange layout (kernels_persist_wide.hip,
+ * csrc/wide_layout.h) for a group of `rows_per_group` rows (1..16): returns the number of
+ * violations (0 = every producer packet of a hop lands on exactly the consumer packet that
+ * expects its (row, unit quad), aligned, inside its slot; no-packet offsets out of range),
+ * or WRNN_ERR_INVALID. No device needed. */
+int wrnn_debug_wide_layout(int rows_per_group);
+
 /* Raw access for tests: copy the RAW noise (seq_len, rows, n_classes) of the last call's
  * first `n_steps` steps to host (float32). */
 int wrnn_debug_noise(wrnn_handle* h, int n_steps, float* out, size_t capacity);

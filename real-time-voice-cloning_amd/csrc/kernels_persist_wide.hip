@@ -29,6 +29,9 @@
 #include "wrnn_kernels.h"
 #include "persist_common.h"
 #include "philox.h"
+#include "wide_layout.h"
+
+#include <vector>
 
 namespace wrnn {
 
@@ -41,13 +44,15 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // of k-steps 4p..4p+3 (k-step ks of k-slot c is unit 64 e + 16 c + ks: the weight images' order,
 // runtime.hip pack_persist_wide) -- then room for 1024 more floats. Untagged: a slot not yet written for
 // the step holds the sentinel kSent (see pub / w_poll).
-constexpr int WS_MAIN = 8 * 4 * 64 * 4;
-constexpr int WSLOT = WS_MAIN + 1024;
-constexpr int WV = 2 * WSLOT;
+// (wide_layout.h: the formulas, shared with the host-side check wide_layout_check)
+using wide::WS_MAIN;
+using wide::WSLOT;
+using wide::WV;
+using wide::WX_D;
+using wide::WX_GROUP;
 constexpr unsigned kSent = 0x7fbadbadu;  // a signalling NaN: no arithmetic result is ever this
 enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
-constexpr int WX_D = WB_N * WV;                    // candidates [n 16][slot 32] (value, tag|class)
-constexpr int WX_GROUP = WX_D + 16 * 32 * 2 + 64;
+static_assert(WB_N == wide::kBufs, "one slot pair per published vector");
 // Per-group operand ring (PersistArgs::wring, runtime.hip persist_wide_ring_floats): P1 (r, z, n of
 // W_ih1 (I c) + b_ih1, then I c + b_I) and the Gumbel noise of every cell for 4 steps,
 // [slot = step & 3][row n][unit / class], formed in-kernel three steps ahead (see the fc3 window)
@@ -121,7 +126,7 @@ __device__ __forceinline__ void wbar() {
 // w_issue alone: the first round issued early, for an off-path operand published long before
 // its use, checked later by w_poll with pre = true.
 __device__ __forceinline__ void w_issue(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4]) {
-    unsigned vo = valid ? voff : 0x80000000u;
+    unsigned vo = valid ? voff : wide::kNoOffset;
     asm volatile("" : "+v"(vo));
 #pragma unroll
     for (int i = 0; i < 4; ++i) cc[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
@@ -129,14 +134,15 @@ __device__ __forceinline__ void w_issue(rsrc_t xr, unsigned voff, unsigned so, b
 // Packet i of a poll round alone (see w_issue): issued into a packet register an off-path
 // product has finished reading, so a critical hop's first round needs no extra registers.
 __device__ __forceinline__ void w_issue1(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v& c, int i) {
-    unsigned vo = valid ? voff : 0x80000000u;
+    unsigned vo = valid ? voff : wide::kNoOffset;
     asm volatile("" : "+v"(vo));
     c = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024u * i, so, kCpNT);
 }
-// On a timeout the first poller records its site in PC_WHERE (`where`: site << 28 | slot << 22 |
-// step; the wave is added here) and whether its packets were missing, for the error message.
+// On a timeout the first poller records its site in PC_WHERE (`where`: site << 28 | slot << 22;
+// the wave is added here), whether its packets were missing (PC_WHERE + 1) and the step
+// (PC_WHERE + 2, all 32 bits), for the error message.
 __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bool valid, u4v (&cc)[4],
-                                       unsigned* ctl, unsigned where, bool pre = false) {
+                                       unsigned* ctl, unsigned where, unsigned step, bool pre = false) {
     const unsigned t0 = p_now();
     unsigned nsp = 0;
     if (!pre) w_issue(xr, voff, so, valid, cc);
@@ -164,8 +170,10 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 #pragma unroll
                 for (int i = 0; i < 4; ++i) mok &= p_ready(cc[i]);
                 const bool mbad = !__all(mok);
-                if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | ((threadIdx.x >> 6) << 19)) == 0u)
+                if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | ((threadIdx.x >> 6) << 19)) == 0u) {
                     ctl[PC_WHERE + 1] = mbad ? 1u : 0u;
+                    ctl[PC_WHERE + 2] = step;
+                }
             }
             if ((threadIdx.x & 63) == 0) atomicMax(ctl + PC_ERR, 2u);
             return false;
@@ -200,8 +208,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     const bool cell = tid < 16 * R;
     const int cu = 16 * w + cul;
     const int crow = g0 + kPG * (cell ? cn : 0);
-    int t_now = 0;  // (for the timeout site record, PC_WHERE)
-    auto wh = [&](unsigned site) { return site << 28 | (unsigned)w << 22 | ((unsigned)t_now & 0x7ffffu); };
+    // timeout site record (PC_WHERE): site << 28 | slot << 22 (| wave << 19, added by the poller);
+    // the step goes to PC_WHERE + 2 whole
+    auto wh = [&](unsigned site) { return site << 28 | (unsigned)w << 22; };
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * WX_GROUP);
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
@@ -253,32 +262,30 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     // byte offsets in a slot: this lane's packet 0 (consumer); the packet of the unit quad
     // cul .. cul + 3 of row cn (producer: lane cul % 4 == 0 of the quad gathers and publishes;
     // slot w = wave e = w / 4, k-slot c = w % 4, packet p = cul / 4)
-    const unsigned o_cons = (unsigned)((v * 4 * 64 + l) * 16);
-    const unsigned o_prod = (unsigned)((((w >> 2) * 4 + (cul >> 2)) * 64 + 16 * (w & 3) + cn) * 16);
+    const unsigned o_cons = wide::cons_off(v, l);
+    const unsigned o_prod = wide::prod_off(w, cn, cul);
     // publish the cell's value of step s: slot s & 1, and the sentinel into slot (s + 1) & 1
     // every wave and lane issues the publish stores; a lane that does not publish stores to an
     // out-of-range offset (dropped by the buffer range check), so every path through a stage
     // carries the same stores and a poll issued before them need not wait for their acks
     auto pub_if = [&](bool on, int hb, float val, unsigned s) {
         const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
-        const unsigned vo = on && cell && (cul & 3) == 0 ? o_prod : 0x80000000u;
-        const unsigned sb = (unsigned)(hb * WV) * 4u;
+        const unsigned vo = on && cell && (cul & 3) == 0 ? o_prod : wide::kNoOffset;
         __builtin_amdgcn_raw_buffer_store_b128(
             (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr, vo,
-            sb + (s & 1u) * (unsigned)WSLOT * 4u, 0);
+            wide::slot_base(hb, s), 0);
         __builtin_amdgcn_raw_buffer_store_b128((u4v){kSent, kSent, kSent, kSent}, xr, vo,
-                                               sb + ((s + 1u) & 1u) * (unsigned)WSLOT * 4u, 0);
+                                               wide::slot_base(hb, s + 1u), 0);
     };
     auto pub = [&](int hb, float val, unsigned s) {
         // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]: quad lane 0 receives lanes 1, 2, 3
         const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
         if (cell && (cul & 3) == 0) {
-            const unsigned sb = (unsigned)(hb * WV) * 4u;
             __builtin_amdgcn_raw_buffer_store_b128(
                 (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr, o_prod,
-                sb + (s & 1u) * (unsigned)WSLOT * 4u, 0);
+                wide::slot_base(hb, s), 0);
             __builtin_amdgcn_raw_buffer_store_b128((u4v){kSent, kSent, kSent, kSent}, xr, o_prod,
-                                                   sb + ((s + 1u) & 1u) * (unsigned)WSLOT * 4u, 0);
+                                                   wide::slot_base(hb, s + 1u), 0);
         }
     };
     const rsrc_t fcr = mk_rsrc(a.fcond);
@@ -392,18 +399,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     pub(WB_H1, __builtin_canonicalizef(h1r), (unsigned)a.t0 + 1u);
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
     for (int t = a.t0; t < a.t1; ++t) {
-        t_now = t;
         const unsigned seq = (unsigned)t + 1u;
-        const unsigned slot = (seq & 1u) * (unsigned)WSLOT * 4u;
-        const unsigned so_x1 = (unsigned)(WB_X1 * WV) * 4u + slot, so_h1 = (unsigned)(WB_H1 * WV) * 4u + slot;
-        const unsigned so_x2 = (unsigned)(WB_X2 * WV) * 4u + slot, so_h2 = (unsigned)(WB_H2 * WV) * 4u + slot;
-        const unsigned so_y1 = (unsigned)(WB_Y1 * WV) * 4u + slot, so_y2 = (unsigned)(WB_Y2 * WV) * 4u + slot;
+        const unsigned so_x1 = wide::slot_base(WB_X1, seq), so_h1 = wide::slot_base(WB_H1, seq);
+        const unsigned so_x2 = wide::slot_base(WB_X2, seq), so_h2 = wide::slot_base(WB_H2, seq);
+        const unsigned so_y1 = wide::slot_base(WB_Y1, seq), so_y2 = wide::slot_base(WB_Y2, seq);
         u4v cc[4];
         bool fail = false;
         float x2s = 0.f;  // the value a lo wave publishes (x2, then y1)
         WSTAMP(0);
         // ================= hop E -> stage A: W_ih2[:, :512] x1 (critical) ==================
-        fail |= !w_poll(xr, o_cons, so_x1, bvalid, cc, a.ctl, wh(1));
+        fail |= !w_poll(xr, o_cons, so_x1, bvalid, cc, a.ctl, wh(1), (unsigned)t);
         prefetch(t);
         WSTAMP(1);
         {
@@ -414,6 +419,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) acc[j] = mfma4(WR(j, ks), b, acc[j]);
             }
+            // PA still holds the W_hh2 h2 partials of step t - 1, which waves 0-3 read in their
+            // hop D (gh2, after the candidate store). Waves 4-7 poll x1 of OTHER slots only
+            // (wave v: slots 4v .. 4v + 3), so nothing orders those reads before this store but
+            // a barrier: every wave reaches it after its hop-E poll anyway.
+            wbar();
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 *reinterpret_cast<v4f*>(lds + WL_PA + ((v * 3 + j) * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
@@ -447,7 +457,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         WSTAMP(3);
         // ================= W_hh1 h1 -> gh1 partials (off-path, hop A wait) ==================
         {
-            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl, wh(2), true);
+            fail |= !w_poll(xr, o_cons, so_h1, bvalid, cc, a.ctl, wh(2), (unsigned)t, true);
             WXSTAMP(26);
             v4f acc[3] = {(v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}, (v4f){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -465,7 +475,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WXSTAMP(27);
         // ================= hop A -> stage B: fc1 x2 (critical) =============================
-        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3), true);
+        fail |= !w_poll(xr, o_cons, so_x2, bvalid, cc, a.ctl, wh(3), (unsigned)t, true);
         // h2 (published with x2, just read) loads now: in flight over fc1 and its epilogue
         u4v ch[4];
         w_issue(xr, o_cons, so_h2, bvalid, ch);
@@ -499,7 +509,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         // ================= W_hh2 h2 -> gh2 partials (off-path, hop B wait) ==================
         {
             WXSTAMP(28);
-            fail |= !w_poll(xr, o_cons, so_h2, bvalid, ch, a.ctl, wh(5), true);
+            fail |= !w_poll(xr, o_cons, so_h2, bvalid, ch, a.ctl, wh(5), (unsigned)t, true);
 #pragma unroll
             for (int i = 0; i < 4; ++i) cc[i] = ch[i];
             WXSTAMP(29);
@@ -523,7 +533,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         WXSTAMP(30);
         // ================= hop B -> stage C: fc2 y1 (critical) =============================
-        fail |= !w_poll(xr, o_cons, so_y1, bvalid, cc, a.ctl, wh(6));
+        fail |= !w_poll(xr, o_cons, so_y1, bvalid, cc, a.ctl, wh(6), (unsigned)t);
         WSTAMP(6);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -550,7 +560,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             pub(WB_Y2, y, seq);
         }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
-        fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl, wh(8));
+        fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl, wh(8), (unsigned)t);
         prefetch_d(t);
         WSTAMP(8);
         {
@@ -584,12 +594,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 row16_argmax(val, cls);
                 if (cell && cul == 0)
                     __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls},
-                                                          xr, (unsigned)((cn * 32 + w) * 2) * 4u, WX_D * 4, 0);
+                                                          xr, wide::cand_off(cn, w), WX_D * 4, 0);
             }
             // gh1 = W_hh1 h1 + b_hh1 (for GRU1 below) and gh2 = W_hh2 h2 + b_hh2 (the next GRU2)
             // from the off-path partials, while the candidates travel: every wave wrote them
-            // before the stage C barrier, and they are rewritten only after this workgroup's
-            // x1 publish (PH: next hop A wait; PA: next stage A, behind the x1 hop)
+            // before the stage C barrier. PH is rewritten in the next hop-A wait, after the next
+            // stage-A barrier; PA in the next stage A behind a barrier of its own (see there):
+            // this wave reaches both only after these reads have completed.
             if (cell) {
                 float gs[6];
 #pragma unroll
@@ -618,13 +629,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 unsigned nsp = 0;
                 while (true) {
                     if (cell) {
-                        unsigned vo = (unsigned)((cn * 32 + 2 * cul) * 2) * 4u;
+                        unsigned vo = wide::cand_off(cn, 2 * cul);
                         asm volatile("" : "+v"(vo));
                         q = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, WX_D * 4, kCpNT);
                     }
                     if (__all((q.y >> 11) == want && (q.w >> 11) == want)) break;
                     if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
-                        if (l == 0 && !ld_sc1_u(a.ctl + PC_ERR)) atomicCAS(a.ctl + PC_WHERE, 0u, wh(9) | ((unsigned)v << 19));
+                        if (l == 0 && !ld_sc1_u(a.ctl + PC_ERR) &&
+                            atomicCAS(a.ctl + PC_WHERE, 0u, wh(9) | ((unsigned)v << 19)) == 0u)
+                            a.ctl[PC_WHERE + 2] = (unsigned)t;
                         if (l == 0) atomicMax(a.ctl + PC_ERR, 2u);
                         fail = true;
                         break;
@@ -694,13 +707,61 @@ __global__ __launch_bounds__(256) void k_wide_xbuf_reset(uint4* x) {
     const unsigned f = (unsigned)((i * 4) % WX_GROUP);
     x[i] = f >= (unsigned)WX_D ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(kSent, kSent, kSent, kSent);
 }
-static_assert(WX_GROUP % 4 == 0 && WX_D % 4 == 0, "reset works in 16-byte units");
 hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s) {
     const unsigned n = (unsigned)((size_t)kPG * WX_GROUP / 4);
     k_wide_xbuf_reset<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<uint4*>(xbuf));
     return hipGetLastError();
 }
 size_t persist_wide_ring_floats() { return (size_t)kPG * WR_GROUP; }
+
+// Exhaustive host-side check of the exchange layout for a group of R rows (wide_layout.h): the
+// producer packets of one hop slot (32 slots x R rows x 4 unit quads) and the consumer packets
+// (8 waves x 64 lanes x 4 packets, lanes of rows >= R off) are the same set, each once, every
+// matched pair carries the same (row, unit quad), all 16-byte aligned inside the slot's main
+// region; slots of different buffers / parities never overlap; the candidates fit their area;
+// the no-packet offset fails the range check for every slot base. Returns the violations.
+int wide_layout_check(int R) {
+    using namespace wide;
+    if (R < 1 || R > kRows) return -1;
+    int bad = 0;
+    std::vector<int> owner(WS_MAIN / 4, -1);  // packet index -> producer id
+    for (int w = 0; w < kSlots; ++w)
+        for (int cn = 0; cn < R; ++cn)
+            for (int cul = 0; cul < 16; cul += 4) {
+                const unsigned o = prod_off(w, cn, cul);
+                if (o % 16 || o + 16 > (unsigned)WS_MAIN * 4u) { ++bad; continue; }
+                int& ow = owner[o / 16];
+                if (ow >= 0) ++bad;  // two producers on one packet
+                ow = (w * kRows + cn) * 16 + cul;
+            }
+    int matched = 0;
+    for (int v = 0; v < kWaves; ++v)
+        for (int l = 0; l < 64; ++l) {
+            if (cons_row(l) >= R) continue;  // polls kNoOffset (w_issue)
+            for (int i = 0; i < kPackets; ++i) {
+                const unsigned o = cons_off(v, l) + 1024u * (unsigned)i;
+                if (o % 16 || o + 16 > (unsigned)WS_MAIN * 4u) { ++bad; continue; }
+                const int ow = owner[o / 16];
+                if (ow < 0) { ++bad; continue; }  // nobody publishes what this lane waits for
+                const int w = ow / (kRows * 16), cn = (ow / 16) % kRows, cul = ow % 16;
+                if (cn != cons_row(l) || 16 * w + cul != cons_unit0(v, l, i)) ++bad;
+                ++matched;
+            }
+        }
+    if (matched != kSlots * R * 4) ++bad;  // a publication nobody reads
+    // buffer / parity slots: disjoint, inside [0, WX_D); the candidate area after them
+    for (int hb = 0; hb < kBufs; ++hb)
+        for (unsigned s = 0; s < 2; ++s) {
+            const unsigned b = slot_base(hb, s);
+            if (b != (unsigned)(hb * 2 + (int)s) * (unsigned)WSLOT * 4u) ++bad;
+            if (b + (unsigned)WSLOT * 4u > (unsigned)WX_D * 4u) ++bad;
+            if ((unsigned long long)kNoOffset + b + 1024ull * kPackets <= kRsrcRecords) ++bad;
+        }
+    for (int n = 0; n < R; ++n)
+        for (int w = 0; w < kSlots; w += 2)
+            if (cand_off(n, w) + 16 > (unsigned)WX_CAND * 4u || cand_off(n, w) % 16) ++bad;
+    return bad;
+}
 size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
 size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
 

@@ -137,7 +137,8 @@ struct wrnn_handle {
     // captured CHAIN graphs (their k_sample arguments hold the buffers)
     std::vector<int> dbg_steps;
     DevBuf dbg_out, dbg_map;
-    int dbg_gen = 0, dbg_rows = 0, dbg_S = 0;
+    uint64_t dbg_gen = 0;  // its own graph-key field (no shifted int: ADVICE r3)
+    int dbg_rows = 0, dbg_S = 0;
     DbgLogits dbg{};
 
     // ---- device weights
@@ -171,7 +172,7 @@ struct wrnn_handle {
         size_t mel_in_cap = 0;
     } ws;
     // captured recurrence chunks: (t0, len, S if last chunk else -1, rows, timing, MOL seed)
-    std::map<std::tuple<int, int, int, int, int, uint64_t>, hipGraphExec_t> graphs;
+    std::map<std::tuple<int, int, int, int, int, uint64_t, uint64_t>, hipGraphExec_t> graphs;
 
     // ---- call state
     int last_B = 0, last_S = 0, last_L0 = 0, last_T0 = 0;
@@ -1487,8 +1488,8 @@ int run_chunk(wrnn_handle* h, int t0, int len, int S) {
     const bool last = t0 + len >= S;
     const int key_S = last ? S : -1;
     auto key = std::make_tuple(t0, len, key_S, h->last_B,
-                               (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1) | (h->dbg_gen << 24),
-                               h->cfg.mode != WRNN_MODE_RAW ? h->seed : (uint64_t)0);
+                               (h->timing ? 1 : 0) | ((h->phase_step + 1) << 1),
+                               h->cfg.mode != WRNN_MODE_RAW ? h->seed : (uint64_t)0, h->dbg_gen);
     auto it = h->graphs.find(key);
     if (it == h->graphs.end()) {
         hipGraph_t g;
@@ -2026,7 +2027,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         static const char* what[] = {"", "workgroups did not become co-resident",
                                      "exchange timeout", "workgroups not spread 32 per XCD",
                                      "aborted"};
-        unsigned wh[2] = {0, 0};
+        unsigned wh[3] = {0, 0, 0};
         (void)hipMemcpy(wh, (unsigned*)P.ctl.p + PC_WHERE, sizeof(wh), hipMemcpyDeviceToHost);
         const unsigned where = wh[0];
         if (where && std::getenv("WRNN_DEBUG_WHERE"))
@@ -2036,7 +2037,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         if (where)  // kernels_persist_wide.hip: the first timeout's site (PC_WHERE)
             msg += " (site " + std::to_string(where >> 28) +
                    ", slot " + std::to_string((where >> 22) & 31) + ", wave " + std::to_string((where >> 19) & 7) +
-                   ", step " + std::to_string(where & 0x7ffff) + ")";
+                   ", step " + std::to_string(wh[2]) + ")";
         fail(WRNN_ERR_HIP, msg);
         return kPersistFallback;
     }
@@ -2071,6 +2072,13 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     return WRNN_OK;
 }
 
+// Captured CHAIN graphs are keyed by their launch arguments; those that hold buffers which
+// are about to change are destroyed rather than kept unreachable.
+static void drop_graphs(wrnn_handle* h) {
+    for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+    h->graphs.clear();
+}
+
 // Logit capture of this call (wrnn_set_debug_steps): map[t] = slot of step t (or -1), the
 // capture buffer NaN-filled so an unwritten entry shows. Off: null pointers in every launch.
 int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
@@ -2078,7 +2086,10 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
     const void* out0 = h->dbg_out.p;
     const void* map0 = h->dbg_map.p;
     if (!on) {
-        if (h->dbg.out) ++h->dbg_gen;
+        if (h->dbg.out) {
+            ++h->dbg_gen;
+            drop_graphs(h);  // graphs captured with capture buffers in their k_sample arguments
+        }
         h->dbg = DbgLogits{};
         h->dbg_rows = 0;
         return WRNN_OK;
@@ -2091,7 +2102,10 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
         if (h->dbg_steps[k] < S) map[h->dbg_steps[k]] = (int)k;
     HIPC(hipMemcpyAsync(h->dbg_map.p, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
     HIPC(hipMemsetAsync(h->dbg_out.p, 0xff, n_out * sizeof(float), h->stream));  // NaN
-    if (!h->dbg.out || out0 != h->dbg_out.p || map0 != h->dbg_map.p) ++h->dbg_gen;
+    if (!h->dbg.out || out0 != h->dbg_out.p || map0 != h->dbg_map.p) {
+        ++h->dbg_gen;
+        drop_graphs(h);  // their k_sample arguments may hold the old capture buffers
+    }
     h->dbg.out = h->dbg_out.f();
     h->dbg.map = (const int*)h->dbg_map.p;
     h->dbg_rows = Bp;
@@ -2103,6 +2117,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
                   wrnn_progress_fn cb, void* user) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    // explicit per-utterance noise streams (wrnn_set_utt_streams) belong to this call whatever
+    // its outcome: taken before any early return, so a failed call never leaves them armed for
+    // an unrelated next one
+    std::vector<uint32_t> ustreams;
+    ustreams.swap(h->utt_streams);
     if (!h->finalized)
         return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
     if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
@@ -2136,9 +2155,6 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         Tmax = std::max(Tmax, p.T);
     }
     if (B > 4096) return fail(WRNN_ERR_INVALID, "too many rows in one call (max 4096)");
-    // explicit per-utterance noise streams (wrnn_set_utt_streams) are consumed by this call
-    std::vector<uint32_t> ustreams;
-    ustreams.swap(h->utt_streams);
     if (!ustreams.empty() && (int)ustreams.size() != n_utts)
         return fail(WRNN_ERR_INVALID, "wrnn_set_utt_streams gave " + std::to_string(ustreams.size()) +
                                           " streams for a call of " + std::to_string(n_utts) + " utterances");
@@ -2735,6 +2751,12 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
     if (bytes) *bytes = by;
     if (flops) *flops = fl;
     return WRNN_OK;
+}
+
+int wrnn_debug_wide_layout(int rows_per_group) {
+    const int bad = wide_layout_check(rows_per_group);
+    if (bad < 0) return fail(WRNN_ERR_INVALID, "rows_per_group must be 1..16");
+    return bad;
 }
 
 int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,

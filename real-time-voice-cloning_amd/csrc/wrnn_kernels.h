@@ -181,8 +181,9 @@ constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
 
 // control words (zeroed by the host before every launch); PC_ERR: 1 registration timeout,
 // 2 exchange timeout, 3 workgroups not spread 32 per XCD
-// PC_WHERE: the first exchange timeout's site (wide kernel: site << 28 | slot << 22 | wave << 19 |
-// step), reported in the error message; PC_WHERE + 1: whether that poll's packets were missing
+// PC_WHERE: the first exchange timeout's site (wide kernel: site << 28 | slot << 22 | wave << 19),
+// reported in the error message; PC_WHERE + 1: whether that poll's packets were missing;
+// PC_WHERE + 2: its step
 enum PersistCtl : int { PC_REG = 0, PC_TOTAL = 8, PC_ERR = 9, PC_WHERE = 10, PC_WORDS = 16 };
 // progress cadence of the reference's callback (fatchord_version.py:234: i % 100 == 0)
 constexpr int kProgressEvery = 100;
@@ -254,6 +255,7 @@ size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
 int persist_wide_scratch();
+int wide_layout_check(int rows_per_group);  // host: violations of the exchange layout (wide_layout.h)
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise
 // ---------------------------------------------------------------------------------------

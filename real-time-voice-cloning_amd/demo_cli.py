@@ -66,6 +66,10 @@ def main():
     ap.add_argument("--vocoder-type", default="fatchord-wavernn")
     ap.add_argument("--repeat", type=int, default=2,
                     help="timed passes over the same utterances; the last one is reported")
+    ap.add_argument("--dump", default=None,
+                    help="write rank 0's first utterance as the vocoder saw it (normalised mel, "
+                         "fold-row labels, seed, noise stream) to this .npz: the GPU parity check of "
+                         "the end-to-end run against the oracle (tests/test_gpu_e2e.py)")
     ap.add_argument("--warmup", type=int, default=1,
                     help="untimed passes of a short utterance through the three models first "
                          "(library and kernel initialisation), as a serving process would")
@@ -160,6 +164,14 @@ def main():
                     for s in specs]
             wavs = model.generate_batch(mels, True, hpv.gen_target, hpv.gen_overlap, hpv.mu_law,
                                         sp.preemphasize, streams=[base + i for i in mine])
+            if args.dump and rank == 0:
+                rows = model.last_batch_rows
+                nb = model.fold_shape(int(mels[0].shape[1]), True, hpv.gen_target, hpv.gen_overlap)[0]
+                np.savez(args.dump, mel=mels[0].cpu().numpy(), rows=rows[:nb], wav=wavs[0],
+                         seed=np.int64(args.seed if args.seed is not None else -1),
+                         stream=np.int64(base + mine[0]), utterance=np.int64(mine[0]),
+                         model_type=np.array(model.model_type),
+                         weights_seed=np.int64(rw + 2 if rw is not None else -1))
         model.set_stream(base + args.utterances)
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()

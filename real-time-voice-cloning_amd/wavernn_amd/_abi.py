@@ -39,7 +39,7 @@ EXPORTED = [
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
     'wrnn_debug_beta', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
-    'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits',
+    'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits', 'wrnn_debug_wide_layout',
 ]
 
 
@@ -137,6 +137,7 @@ def load_library(path=None):
                                         P(ctypes.c_float), c_size_t]),
         'wrnn_debug_p1': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
         'wrnn_set_debug_steps': (c_int, [c_void_p, P(c_int), c_int]),
+        'wrnn_debug_wide_layout': (c_int, [c_int]),
         'wrnn_debug_logits': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
     }
     for name, (res, args) in sig.items():

@@ -96,3 +96,15 @@ def test_beta_mode_is_geneing_only():
     h = ctypes.c_void_p()
     assert lib.wrnn_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == _abi.WRNN_ERR_INVALID
     assert b'geneing' in lib.wrnn_last_error()
+
+
+def test_wide_exchange_layout_exhaustive():
+    """csrc/wide_layout.h, checked by the library's own host code for every row count of a wide
+    group: each producer packet of a hop lands on exactly the consumer packet that expects its
+    (row, unit quad), aligned, inside its slot; no-packet offsets fail the range check
+    (the round-3 18-row deadlock)."""
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    assert [lib.wrnn_debug_wide_layout(r) for r in range(1, 17)] == [0] * 16
+    assert lib.wrnn_debug_wide_layout(0) == _abi.WRNN_ERR_INVALID
+    assert lib.wrnn_debug_wide_layout(17) == _abi.WRNN_ERR_INVALID

@@ -91,3 +91,33 @@ def test_default_plan_uses_wide_launch_for_c4_rows():
     assert roff[-1] == 144
     names = _stage_names(m)
     assert 'persist_wide' in names, names
+
+
+def test_wide_every_rows_per_group_matches_register_resident(monkeypatch):
+    """Every group fill of the wide launch, 1..16 rows per group, with padding rows in some
+    groups (8 R - R % 3 unbatched 1-row utterances): the wide kernel's labels equal the
+    register-resident kernel's (itself pinned to the oracle) row for row. The row counts the
+    round-3 18-row instance deadlocked at do not exist in the shipped kernel (<= 16); this covers
+    the shipped instance's."""
+    import torch
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_raw9_tiny')
+    m, hp, sd = make_model(meta)
+    m.set_engine('persist')
+    m.enable_stage_timing(True)
+    for R in range(1, 17):
+        n = 8 * R - R % 3
+        dev = [torch.from_numpy((synth_mel(6, 700 + u) / sp.max_abs_value).astype(np.float32)).cuda()
+               for u in range(n)]
+        out = {}
+        for wide in ('1', '0'):
+            monkeypatch.setenv('WRNN_PERSIST_WIDE', wide)
+            m.set_seed(meta['noise_seed'])
+            lab, roff, S = m.generate_batch_device(dev, False, 0, 0)
+            names = _stage_names(m)
+            assert ('persist_wide' in names) == (wide == '1'), (R, wide, names)
+            out[wide] = lab.cpu().numpy()
+        d = np.argwhere(out['1'] != out['0'])
+        assert len(d) == 0, f'R={R} ({n} rows): first divergence {d[np.argmin(d[:, 1])]}'
