@@ -847,15 +847,17 @@ hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// RAW Gumbel noise of every (step, row, class): philox.h gumbel_of
-__global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int ng,
+// RAW Gumbel noise of every (step, row, class) of rows [r0, r0 + nrows) of the [S][ld][n]
+// buffer: philox.h gumbel_of (wide launches form theirs in-kernel, so a plan with them fills
+// only the register-resident launches' rows)
+__global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int r0, int nrows, int ld, int ng,
                                                 const RowInfo* rows, uint32_t k0, uint32_t k1) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r, k4)
     const size_t total = (size_t)S * nrows * ng;
     if (i >= total) return;
     const int k4 = (int)(i % ng);
     const size_t tr = i / ng;
-    const int r = (int)(tr % nrows), t = (int)(tr / nrows);
+    const int r = r0 + (int)(tr % nrows), t = (int)(tr / nrows);
     const RowInfo ri = rows[r];
     const U4 o = philox4x32_10((uint32_t)k4, (uint32_t)t, (uint32_t)ri.fold, ri.stream, k0, k1);
     float4 v;
@@ -863,17 +865,22 @@ __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int nrows, int
     v.y = gumbel_of(o.y);
     v.z = gumbel_of(o.z);
     v.w = gumbel_of(o.w);
-    g[i] = v;
+    g[((size_t)t * ld + r) * ng + k4] = v;
 }
 
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
                          uint32_t k0, uint32_t k1, hipStream_t s) {
-    if (n_classes % 4) return hipErrorInvalidValue;
+    return launch_gumbel_rows(g, S, 0, nrows, nrows, n_classes, rows, k0, k1, s);
+}
+
+hipError_t launch_gumbel_rows(float* g, int S, int r0, int nrows, int ld, int n_classes,
+                              const RowInfo* rows, uint32_t k0, uint32_t k1, hipStream_t s) {
+    if (n_classes % 4 || r0 < 0 || r0 + nrows > ld) return hipErrorInvalidValue;
     const int ng = n_classes / 4;
     const size_t total = (size_t)S * nrows * ng;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gumbel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<float4*>(g), S, nrows, ng, rows, k0, k1);
+                       reinterpret_cast<float4*>(g), S, r0, nrows, ld, ng, rows, k0, k1);
     return hipGetLastError();
 }
 

@@ -354,6 +354,8 @@ hipError_t launch_mol_noise(float* out, int S, int nrows, const RowInfo* rows, u
                             uint32_t k1, hipStream_t s);
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
                          uint32_t k0, uint32_t k1, hipStream_t s);
+hipError_t launch_gumbel_rows(float* g, int S, int r0, int nrows, int ld, int n_classes,
+                              const RowInfo* rows, uint32_t k0, uint32_t k1, hipStream_t s);
 // ring: the P1-ring variant (PersistArgs::p1q set) or the P1-stream variant
 int persist_variant_ok(int nr, int cpw, int mode, int ring);
 int persist_variant_scratch(int nr, int cpw, int mode, int ring);
