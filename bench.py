@@ -360,7 +360,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             us = float(t.item())
         achieved = by / (us * 1e-6) / 1e9 if us > 0 else None
-        kernel = {'persist': 'k_persist', 'persist_wide': 'k_persist_wide'}.get(name, f'k_stage<{name}>')
+        sfx = {'runtimeracer-wavernn': '_rr', 'geneing-wavernn': '_gen'}.get(args.model, '')
+        kernel = {'persist': 'k_persist' + sfx, 'persist_wide': 'k_persist_wide' + sfx}.get(name, f'k_stage<{name}>')
         roof = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': None,

@@ -202,6 +202,7 @@ struct wrnn_handle {
         const float *p1taps = nullptr, *zero_np = nullptr;
         int p1split = -1;  // phase from which the 4 in-kernel taps start at frame f - 1
         const float *wwide = nullptr, *wwide_lds = nullptr;  // wide-row launches (MFMA images)
+        const float* wwide_rr = nullptr;  // runtimeracer wide-row launches (kernels_persist_wide_rr.hip)
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
@@ -537,6 +538,7 @@ int pack_p1(wrnn_handle* h, bool x4) {
 }
 
 int pack_persist_wide(wrnn_handle* h);
+int pack_persist_wide_rr(wrnn_handle* h);
 
 int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     auto& T = h->host;
@@ -736,7 +738,59 @@ int pack_persist_rr(wrnn_handle* h, int oG3, int oF1, int oF3) {
     P.oG2 = oG3;
     P.oF1 = oF1;
     P.oF2 = oF3;
+    CHECK(pack_persist_wide_rr(h));
     P.ok = true;
+    return WRNN_OK;
+}
+
+// Runtimeracer wide-row launch weight images (kernels_persist_wide_rr.hip): MFMA A operands.
+// Slot w (half A: w < 16, half B: w >= 16; s = w % 16 owns units 16 s .. 16 s + 15 of its half's
+// layers), wave v, lane l, tile T, k-step ks: W_T[row 16 s + (l & 15)][input 32 v + 8 (l >> 4) + ks]
+// at [w][v][2 T + ks / 4][l] component ks % 4. Tiles of A: W_ih2 r, z, n | W_hh2 r, z, n | W_ih4
+// r, z, n | W_hh4 r, z, n | fc2 | fc4; of B: W_hh1 r, z, n | W_ih3[:, :256] r, z, n | W_hh3 r, z,
+// n | fc1[:, :256] | fc3[:, :256] | fc5 rows cpw s + 16 j + m (j < n / 256), cpw = n / 16.
+int pack_persist_wide_rr(wrnn_handle* h) {
+    auto& T = h->host;
+    auto& P = h->pw;
+    P.wwide_rr = nullptr;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
+    if (h->cfg.mode != WRNN_MODE_RAW || H != kRH || F != kRH || (n != 512 && n != 1024)) return WRNN_OK;
+    const int cpw = n / 16;
+    auto g3 = [&](const char* key, int ld, int t, int u, int k) { return T[key][(size_t)(t * H + u) * ld + k]; };
+    auto elem = [&](int w, int tile, int m, int k) -> float {
+        const int s = w & 15, u = 16 * s + m;
+        if (w < 16) {
+            switch (tile / 3) {
+                case 0: return g3("rnn2.weight_ih_l0", H, tile % 3, u, k);
+                case 1: return g3("rnn2.weight_hh_l0", H, tile % 3, u, k);
+                case 2: return g3("rnn4.weight_ih_l0", H, tile % 3, u, k);
+                case 3: return g3("rnn4.weight_hh_l0", H, tile % 3, u, k);
+                default: return tile == 12 ? T["fc2.weight"][(size_t)u * F + k]
+                                           : tile == 13 ? T["fc4.weight"][(size_t)u * F + k] : 0.f;
+            }
+        }
+        if (tile < 3) return g3("rnn1.weight_hh_l0", H, tile, u, k);
+        if (tile < 6) return g3("rnn3.weight_ih_l0", H + A, tile - 3, u, k);
+        if (tile < 9) return g3("rnn3.weight_hh_l0", H, tile - 6, u, k);
+        if (tile == 9) return T["fc1.weight"][(size_t)u * (H + A) + k];
+        if (tile == 10) return T["fc3.weight"][(size_t)u * (F + A) + k];
+        const int c = cpw * s + 16 * (tile - 11) + m;
+        return tile - 11 < cpw / 16 && c < n ? T["fc5.weight"][(size_t)c * F + k] : 0.f;
+    };
+    std::vector<float> wr(persist_wide_rr_wreg_floats(), 0.f);
+    const int nq = (int)(wr.size() / ((size_t)kPM * 8 * 64 * 4));  // float4 per lane (30)
+    for (int w = 0; w < kPM; ++w)
+        for (int v = 0; v < 8; ++v)
+            for (int l = 0; l < 64; ++l)
+                for (int q = 0; q < nq; ++q)
+                    for (int c = 0; c < 4; ++c) {
+                        const int tile = q / 2, ks = 4 * (q % 2) + c;
+                        wr[((((size_t)w * 8 + v) * nq + q) * 64 + l) * 4 + c] =
+                            elem(w, tile, l & 15, 32 * v + 8 * (l >> 4) + ks);
+                    }
+    int rc = WRNN_OK;
+    P.wwide_rr = upload(h, wr, &rc);
+    CHECK(rc);
     return WRNN_OK;
 }
 
@@ -1133,6 +1187,14 @@ static bool p1_ring_ok(const wrnn_handle* h) {
     if (env && std::atoi(env) == 0) return false;
     return !h->pw.rr && !h->pw.gen && h->pw.p1x4 && h->pw.p1taps_ok && h->pw.p1split >= 0 &&
            p1_frames_enabled();
+}
+
+// The runtimeracer wide kernel forms P1 from the per-frame projections (its A half, for the
+// partner B slot) when the 4-tap form exists; else it reads the [S][B][4H] stream.
+static bool rr_frames_ok(const wrnn_handle* h) {
+    const char* env = std::getenv("WRNN_P1_RING");
+    if (env && std::atoi(env) == 0) return false;
+    return h->pw.rr && h->pw.p1x4 && h->pw.p1taps_ok && h->pw.p1split >= 0 && p1_frames_enabled();
 }
 
 // ---- MelResNet of every utterance of a call as one batch of frame columns ---------------
@@ -1753,7 +1815,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     bool any_wide = false;
     for (const auto& L : h->p_plan) any_wide |= L.wide;
     const size_t xfl = gen  ? persist_gen_xbuf_floats()
-                       : rr ? persist_rr_xbuf_floats()
+                       : rr ? std::max(persist_rr_xbuf_floats(), any_wide ? persist_wide_rr_xbuf_floats() : 0)
                             : std::max(persist_xbuf_floats(), any_wide ? persist_wide_xbuf_floats() : 0);
     CHECK(P.xbuf.alloc(xfl * sizeof(float)));
     CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? 11 * kRH : 6 * H) * sizeof(float)));
@@ -1901,9 +1963,19 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int nb = (int)h->p_plan.size();
     a.wwide = (const float4*)W.wwide;
     a.wwide_lds = (const float4*)W.wwide_lds;
-    if (any_wide) {  // the wide kernel forms P1 and the noise in-kernel into this ring
-        CHECK(P.wring.alloc(persist_wide_ring_floats() * sizeof(float)));
+    if (any_wide) {  // the wide kernels form P1 and the noise in-kernel into this ring
+        CHECK(P.wring.alloc((rr ? persist_wide_rr_ring_floats() : persist_wide_ring_floats()) * sizeof(float)));
         a.wring = P.wring.f();
+        ar.wring = a.wring;
+        ar.wwide = (const float4*)W.wwide_rr;
+        if (rr && rr_frames_ok(h)) {
+            ar.p1q = ws.q4.f();
+            ar.p1a = ws.a4.f();
+            ar.p1taps = W.p1taps + (size_t)h->hop * 8;  // the [hop][4] table
+            ar.p1split = W.p1split;
+        }
+        ar.k0 = k0;
+        ar.k1 = k1;
     }
     if (cb && !h->prog_host) {  // progress word + abort word (kAbortWord), two cache lines
         HIPC(hipHostMalloc((void**)&h->prog_host, 128, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1928,8 +2000,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.t0 = 0;
         a.t1 = S;
         a.prog_base = b * S;
-        if (L.wide)  // sentinel-initialised vector slots (kernels_persist_wide.hip w_poll)
-            HIPC(persist_wide_reset_xbuf(P.xbuf.f(), st));
+        if (L.wide)  // sentinel-initialised vector slots (kernels_persist_wide*.hip polls)
+            HIPC(rr ? persist_wide_rr_reset_xbuf(P.xbuf.f(), st) : persist_wide_reset_xbuf(P.xbuf.f(), st));
         else
             HIPC(hipMemsetAsync(P.xbuf.p, 0, xfl * sizeof(float), st));  // step tags
         // registration words only: an error code from an earlier launch stays visible, so the
@@ -1963,7 +2035,13 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.rb = a.rb;
             ar.stamps = a.stamps;
             ar.prog_base = a.prog_base;
-            le = launch_persist_rr(ar, st);
+            if (L.wide) {
+                PersistRRArgs aw = ar;
+                aw.cpw = n / 16;  // classes per B slot of the wide layout (16 slots per half)
+                le = launch_persist_wide_rr(aw, st);
+            } else {
+                le = launch_persist_rr(ar, st);
+            }
         } else if (L.wide) {
             le = launch_persist_wide(a, st);
         } else {
@@ -2123,6 +2201,10 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
     return WRNN_OK;
 }
 
+// per-step cost of a runtimeracer wide-row launch at 1 row per group, for the launch plan
+// (MI355X, bench HIP events)
+static const double kWideRRUs = 15.0;
+
 int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
                   wrnn_progress_fn cb, void* user) {
@@ -2224,6 +2306,15 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             for (int r = 1; r <= kPNR; ++r)
                 if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw, h->cfg.mode))
                     opts.push_back({r, false, h->pw.gen ? us_gen[r] : us_rr[r]});
+            // runtimeracer wide-row launches (kernels_persist_wide_rr.hip), same env switch as
+            // the fatchord ones: WRNN_PERSIST_WIDE 0 never, 1 only wide, 2 by cost
+            int wmode = 2;
+            if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
+            const bool scratch_ok = persist_wide_rr_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
+            if (h->pw.rr && h->pw.wwide_rr && wmode && scratch_ok) {
+                if (wmode == 1) opts.clear();
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, kWideRRUs + 0.05 * r});
+            }
         }
         if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B
             const int c = std::max(1, std::min(kPNR, std::atoi(env)));
@@ -2287,6 +2378,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
             h->p1_ring = false;
     h->p1_stream = use_p && !h->p1_ring;  // (the wide launches form P1 in-kernel too)
+    if (h->p1_stream && h->pw.rr && rr_frames_ok(h)) {  // runtimeracer: only wide launches
+        bool all_wide = !h->p_plan.empty();                // form P1 in-kernel
+        for (const auto& L : h->p_plan) all_wide &= L.wide;
+        if (all_wide) h->p1_stream = false;
+    }
     // MelResNet frame columns: utterance u at [col0[u], col0[u] + T[u])
     std::vector<int> Ts(n_utts), col0(n_utts);
     int Tsum = 0;
@@ -2764,9 +2860,9 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
 }
 
 int wrnn_debug_wide_layout(int rows_per_group) {
-    const int bad = wide_layout_check(rows_per_group);
-    if (bad < 0) return fail(WRNN_ERR_INVALID, "rows_per_group must be 1..16");
-    return bad;
+    const int bad = wide_layout_check(rows_per_group), bad_rr = wide_rr_layout_check(rows_per_group);
+    if (bad < 0 || bad_rr < 0) return fail(WRNN_ERR_INVALID, "rows_per_group must be 1..16");
+    return bad + bad_rr;
 }
 
 int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,

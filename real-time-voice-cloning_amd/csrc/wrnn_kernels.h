@@ -301,9 +301,29 @@ struct PersistRRArgs {
     unsigned* progress;     // as PersistArgs
     int prog_base;
     DbgLogits dbg;
+    // wide-row launches (kernels_persist_wide_rr.hip): MFMA A-operand images, the per-slot ring
+    // of P1 and noise, P1's per-frame form (as PersistArgs; p1q null: the P1 stream), Philox key
+    const float4* wwide;    // [kPM][8 waves][30 float4][64 lanes]
+    float* wring;           // persist_wide_rr_ring_floats()
+    const float* p1q;
+    const float* p1a;
+    const float* p1taps;
+    int p1split;
+    uint32_t k0, k1;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
+// Wide-row runtimeracer launch (kernels_persist_wide_rr.hip): up to kPWideRows rows per XCD
+// group, the group split into two halves of 16 slots that own 16 units of alternate layers,
+// fp32 MFMA products, RAW categorical with 512 or 1024 classes (cpw = n / 16 per B slot).
+hipError_t launch_persist_wide_rr(const PersistRRArgs& a, hipStream_t s);
+size_t persist_wide_rr_lds_bytes();
+size_t persist_wide_rr_xbuf_floats();
+size_t persist_wide_rr_ring_floats();
+size_t persist_wide_rr_wreg_floats();
+hipError_t persist_wide_rr_reset_xbuf(float* xbuf, hipStream_t s);
+int persist_wide_rr_scratch();
+int wide_rr_layout_check(int rows_per_group);
 
 // ---------------------------------------------------------------------------------------
 // Persistent geneing recurrence (kernels_persist_gen.hip): rnn_dims 256, fc_dims 128; per
