@@ -1786,11 +1786,20 @@ int persist_noise(wrnn_handle* h, int S, hipStream_t st) {
         CHECK(P.gumbel.alloc(sizeof(float)));
         return WRNN_OK;
     }
+    // rows that need the stream: the register-resident launches' (k_persist forming its noise
+    // in-kernel measured 6.52 against 5.93 us per C2 step, DESIGN §3.0: the stream stays)
+    bool any_wide = false, any_reg = false;
+    for (const auto& L : h->p_plan) {
+        any_wide |= L.wide;
+        any_reg |= !L.wide;
+    }
+    if (raw && any_wide && !any_reg) {  // every launch draws its noise in-kernel
+        CHECK(P.gumbel.alloc(sizeof(float)));
+        return WRNN_OK;
+    }
     CHECK(P.gumbel.alloc((size_t)S * Bp * (raw ? n : kMolNoise) * sizeof(float)));
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
     const RowInfo* rows = (const RowInfo*)h->ws.rows.p;
-    bool any_wide = false;
-    for (const auto& L : h->p_plan) any_wide |= L.wide;
     if (raw && any_wide) {
         // the wide launches draw their noise in-kernel (kernels_persist_wide.hip ring): fill
         // only the rows of the register-resident launches (C4: 16 of 144 rows, 3.6 -> 0.4 ms)
@@ -2203,7 +2212,7 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
 
 // per-step cost of a runtimeracer wide-row launch at 1 row per group, for the launch plan
 // (MI355X, bench HIP events)
-static const double kWideRRUs = 15.0;
+static const double kWideRRUs = 12.0;  // 12.39 us at 15-16 rows (profiles/r04/wide_rr/)
 
 int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
@@ -2313,7 +2322,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             const bool scratch_ok = persist_wide_rr_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
             if (h->pw.rr && h->pw.wwide_rr && wmode && scratch_ok) {
                 if (wmode == 1) opts.clear();
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, kWideRRUs + 0.05 * r});
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, kWideRRUs + 0.025 * r});
             }
         }
         if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B

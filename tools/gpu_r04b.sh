@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-4 GPU call: runtimeracer wide tests, k_persist in-kernel-noise A/B, rr bench.
+set -u
+O=gpurun_out/r04/${TAG:-b}
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+run() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name" | tee -a $O/steps.log
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $O/steps.log
+  tail -4 "$O/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+S=${STEPS:-rrtests,ab,rrbench}
+[[ ,$S, == *,rrtests,* ]] && run rrtests 400 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_wide_rr.py -k "golden or every"
+if [[ ,$S, == *,ab,* ]]; then
+  i=0
+  for lib in exp/lib_base.so exp/lib_nlicm.so exp/lib_nz1.so exp/lib_base.so exp/lib_nz1.so; do
+    i=$((i + 1))
+    n=$(basename $lib .so)_$i
+    run ab_$n 200 env WRNN_LIB=$PWD/$lib python bench.py --steps 3 --warmup 1 --cpu-seconds 0
+    grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*\|"ms_per_step": [0-9.]*' $O/ab_$n.log | tr '\n' ' '; echo
+  done
+  run ab_nz1_parity 300 env WRNN_LIB=$PWD/exp/lib_nz1.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fullsize.py -k "c2_full or c4"
+fi
+[[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
+[[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
+exit 0
