@@ -192,15 +192,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
     if (tid == 0) lds[QL_FAIL] = 0.f;
 
     // publish the cell's value of step seq: slot seq & 1, the sentinel into slot (seq + 1) & 1
+    // Every lane of the wave issues both stores (a lane that does not publish uses kNoOff, which
+    // the buffer range check drops): no branch around them, so the compiler's waits after them
+    // stay counted (the fatchord wide kernel's round-3 lesson)
     auto pub = [&](int hb, float val, unsigned seq) {
         const float u1 = pdpp<0x39>(val), u2 = pdpp<0x4E>(val), u3 = pdpp<0x93>(val);
-        if (cell && (cul & 3) == 0) {
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr,
-                o_prod, q_slot(hb, seq), 0);
-            __builtin_amdgcn_raw_buffer_store_b128((u4v){kSentR, kSentR, kSentR, kSentR}, xr, o_prod,
-                                                   q_slot(hb, seq + 1u), 0);
-        }
+        unsigned vo = cell && (cul & 3) == 0 ? o_prod : kNoOff;
+        asm volatile("" : "+v"(vo));
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (u4v){__float_as_uint(val), __float_as_uint(u1), __float_as_uint(u2), __float_as_uint(u3)}, xr, vo,
+            q_slot(hb, seq), 0);
+        __builtin_amdgcn_raw_buffer_store_b128((u4v){kSentR, kSentR, kSentR, kSentR}, xr, vo,
+                                               q_slot(hb, seq + 1u), 0);
     };
     // NT-tile product over a hop's packets into the partial tiles at P (tiles T0 ..)
     auto prod = [&](auto ntc_, int T0, const u4v (&cc)[2], int P) {

@@ -25,6 +25,15 @@ if [[ ,$S, == *,ab,* ]]; then
   done
   run ab_nz1_parity 300 env WRNN_LIB=$PWD/exp/lib_nz1.so python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fullsize.py -k "c2_full or c4"
 fi
+if [[ ,$S, == *,abrr,* ]]; then
+  i=0
+  for lib in exp/lib_rrv1.so exp/lib_rrv2.so exp/lib_rrv1.so exp/lib_rrv2.so; do
+    i=$((i + 1))
+    n=$(basename $lib .so)_$i
+    run abrr_$n 300 env WRNN_LIB=$PWD/$lib python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
+    grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*' $O/abrr_$n.log | tr '\n' ' '; echo
+  done
+fi
 [[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 [[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 exit 0
