@@ -179,6 +179,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
     const unsigned o_own = cell ? o_prod + 4u * (unsigned)(cul & 3) : kNoOff;
     auto wh = [&](unsigned site) { return site << 28 | (unsigned)w << 22; };
     const int ntc = a.cpw / 16;  // fc5 tiles of a B slot (cpw = n / 16 classes: 2 or 4)
+    // phase stamps of the traced step (WRNN_PHASE_STEP), wave 0 of slots 0 (A) and 16 (B)
+    uint32_t* ph = a.phases != nullptr && (w == 0 || w == 16) ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
+#define RS(i) \
+    if (ph != nullptr && t == a.phase_t && tid == 0) ph[(i)] = p_now();
 
     // ---- weights: tile T, k-step ks at wq[2 T + ks / 4] component ks % 4 --------------------
     float4 wq[kWq];
@@ -221,15 +225,29 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         for (int j = 0; j < NT; ++j)
             *reinterpret_cast<v4f*>(lds + P + ((v * NT + j) * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc[j];
     };
-    // a cell's sum of the 8 waves' partials of tile j (fixed order)
-    auto psum = [&](int P, int NT, int j) {
-        float acc = 0.f;
+    // a cell's sums of the 8 waves' partials of tiles j0 .. j0 + K - 1 (fixed order v = 0 .. 7),
+    // every LDS read issued before the first add: at this kernel's register pressure the
+    // scheduler otherwise waits on each read in turn (one LDS latency per partial)
+    auto psums = [&](auto kc, int P, int NT, int j0, float* out) {
+        constexpr int K = decltype(kc)::value;
+        float p[K][8];
 #pragma unroll
-        for (int vv = 0; vv < 8; ++vv) acc += lds[P + ((vv * NT + j) * 16 + cn) * 16 + wsw(cn, cul)];
-        return acc;
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int vv = 0; vv < 8; ++vv) p[k][vv] = lds[P + ((vv * NT + j0 + k) * 16 + cn) * 16 + wsw(cn, cul)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float acc = 0.f;
+#pragma unroll
+            for (int vv = 0; vv < 8; ++vv) acc += p[k][vv];
+            out[k] = acc;
+        }
     };
     using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
     bool fail = false;
     u4v cc[2];
     unsigned ov = 0;
@@ -323,19 +341,24 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
         for (int t = a.t0; t < a.t1; ++t) {
             const unsigned seq = (unsigned)t + 1u;
+            RS(0);
             // ---- A1: x1 -> W_ih2 x1 -> GRU2 -> x2, h2 -------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QX1, seq), bvalid, o_own, cc, ov, a.ctl, wh(1), (unsigned)t);
+            RS(1);
             const float x1v = __uint_as_float(ov);
             prod(I3(), 0, cc, PA_G2);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
+            RS(2);
             if (lds[QL_FAIL] != 0.f) return;
             {
                 float x2 = 0.f;
                 if (cell) {
-                    const float gi0 = p_add(psum(PA_G2, 3, 0), cb[cul]);
-                    const float gi1 = p_add(psum(PA_G2, 3, 1), cb[16 + cul]);
-                    const float gi2 = p_add(psum(PA_G2, 3, 2), cb[32 + cul]);
+                    float ps[3];
+                    psums(I3(), PA_G2, 3, 0, ps);
+                    const float gi0 = p_add(ps[0], cb[cul]);
+                    const float gi1 = p_add(ps[1], cb[16 + cul]);
+                    const float gi2 = p_add(ps[2], cb[32 + cul]);
                     h2r = p_gru(gi0, gi1, gi2, g2r, g2z, g2n, h2r);
                     x2 = p_add(x1v, h2r);
                 }
@@ -344,11 +367,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     pub(QH2, h2r, seq);
                 }
             }
+            RS(3);
             // ---- A2: h2 of every A slot -> W_hh2 h2 (next step's gh2; B runs GRU3) ----------
             fail |= !q_poll(xr, o_cons, q_slot(QH2, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(2), (unsigned)t);
+            RS(4);
             prod(I3(), 3, cc, PA_H2);
+            RS(5);
             // ---- A3: x3 -> W_ih4 x3 -> GRU4 -> x4, h4 --------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QX3, seq), bvalid, o_own, cc, ov, a.ctl, wh(3), (unsigned)t);
+            RS(6);
             const float x3v = __uint_as_float(ov);
             prod(I3(), 6, cc, PA_G4);
             if (fail) lds[QL_FAIL] = 1.f;
@@ -357,12 +384,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             {
                 float x4 = 0.f;
                 if (cell) {
-                    g2r = p_add(psum(PA_H2, 3, 0), cb[48 + cul]);
-                    g2z = p_add(psum(PA_H2, 3, 1), cb[64 + cul]);
-                    g2n = p_add(psum(PA_H2, 3, 2), cb[80 + cul]);
-                    const float gi0 = p_add(psum(PA_G4, 3, 0), cb[96 + cul]);
-                    const float gi1 = p_add(psum(PA_G4, 3, 1), cb[112 + cul]);
-                    const float gi2 = p_add(psum(PA_G4, 3, 2), cb[128 + cul]);
+                    float ps[3];
+                    psums(I3(), PA_G4, 3, 0, ps);
+                    const float gi0 = p_add(ps[0], cb[96 + cul]);
+                    const float gi1 = p_add(ps[1], cb[112 + cul]);
+                    const float gi2 = p_add(ps[2], cb[128 + cul]);
                     h4r = p_gru(gi0, gi1, gi2, g4r, g4z, g4n, h4r);
                     x4 = p_add(x3v, h4r);
                 }
@@ -370,12 +396,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     pub(QX4, x4, seq);
                     pub(QH4, h4r, seq);
                 }
+                if (cell) {
+                    float ps[3];
+                    psums(I3(), PA_H2, 3, 0, ps);
+                    g2r = p_add(ps[0], cb[48 + cul]);
+                    g2z = p_add(ps[1], cb[64 + cul]);
+                    g2n = p_add(ps[2], cb[80 + cul]);
+                }
             }
+            RS(7);
             // ---- A4: h4 of every A slot -> W_hh4 h4 (next step's gh4; B runs fc1) -----------
             fail |= !q_poll(xr, o_cons, q_slot(QH4, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(4), (unsigned)t);
             prod(I3(), 9, cc, PA_H4);
+            RS(8);
             // ---- A5: y1 -> fc2 -> y2 --------------------------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QY1, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(5), (unsigned)t);
+            RS(9);
             prod(I1(), 12, cc, PA_F2);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
@@ -383,16 +419,24 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             {
                 float y = 0.f;
                 if (cell) {
-                    g4r = p_add(psum(PA_H4, 3, 0), cb[144 + cul]);
-                    g4z = p_add(psum(PA_H4, 3, 1), cb[160 + cul]);
-                    g4n = p_add(psum(PA_H4, 3, 2), cb[176 + cul]);
-                    y = p_add(psum(PA_F2, 1, 0), cb[192 + cul]);
+                    float ps[3];
+                    psums(I1(), PA_F2, 1, 0, ps);
+                    y = p_add(ps[0], cb[192 + cul]);
                     y = y > 0.f ? y : 0.f;
                 }
                 if (v < 4) pub(QY2, y, seq);
+                if (cell) {
+                    float ps[3];
+                    psums(I3(), PA_H4, 3, 0, ps);
+                    g4r = p_add(ps[0], cb[144 + cul]);
+                    g4z = p_add(ps[1], cb[160 + cul]);
+                    g4n = p_add(ps[2], cb[176 + cul]);
+                }
             }
+            RS(10);
             // ---- A6: y3 -> fc4 -> y4 --------------------------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QY3, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(6), (unsigned)t);
+            RS(11);
             prod(I1(), 13, cc, PA_F4);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
@@ -400,15 +444,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             {
                 float y = 0.f;
                 if (cell) {
-                    y = p_add(psum(PA_F4, 1, 0), cb[208 + cul]);
+                    float ps[1];
+                    psums(I1(), PA_F4, 1, 0, ps);
+                    y = p_add(ps[0], cb[208 + cul]);
                     y = y > 0.f ? y : 0.f;
                 }
                 if (v < 4) pub(QY4, y, seq);
             }
+            RS(12);
             // ---- idle while B runs fc5, the sample and GRU1: the partner's ring entry of step
             // t + 3 (its slot (t + 3) & 3 last held step t - 1, whose reads ended in step t - 1;
             // the stores drain at this wave's next poll, before any later publication)
             ring_make(t + 3);
+            RS(13);
         }
         if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
     } else {
@@ -445,6 +493,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         }
         for (int t = a.t0; t < a.t1; ++t) {
             const unsigned seq = (unsigned)t + 1u;
+            RS(0);
             // per-step cell operands: conditioning of frame(t) (GRU3, fc1, fc3) now; the
             // ring's noise of step t and P1 of step t + 1 (formed by the partner A slot) after
             // the x2 poll below -- A stored them before that publication
@@ -463,9 +512,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             }
             // ---- B1: h1 of every B slot -> W_hh1 h1 (GRU1 at this step's end; A runs GRU2) -
             fail |= !q_poll(xr, o_cons, q_slot(QH1, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(7), (unsigned)t);
+            RS(1);
             prod(I3(), 0, cc, PB_H1);
+            RS(2);
             // ---- B2: x2 -> W_ih3 x2 -> GRU3 -> x3, h3 ---------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QX2, seq), bvalid, o_own, cc, ov, a.ctl, wh(8), (unsigned)t);
+            RS(3);
             const float x2v = __uint_as_float(ov);
             if (cell) {  // (non-temporal: the ring lines were written by another CU)
                 const unsigned nb = (unsigned)(RG_P + ((t & 3) * kRowsW + cn) * 64 + cul) * 4u;
@@ -481,12 +533,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             {
                 float x3 = 0.f;
                 if (cell) {
-                    g1r = p_add(psum(PB_H1, 3, 0), cb[cul]);
-                    g1z = p_add(psum(PB_H1, 3, 1), cb[16 + cul]);
-                    g1n = p_add(psum(PB_H1, 3, 2), cb[32 + cul]);
-                    const float gi0 = p_add(psum(PB_G3, 3, 0), pc[0]);
-                    const float gi1 = p_add(psum(PB_G3, 3, 1), pc[1]);
-                    const float gi2 = p_add(psum(PB_G3, 3, 2), pc[2]);
+                    float ps[3];
+                    psums(I3(), PB_G3, 3, 0, ps);
+                    const float gi0 = p_add(ps[0], pc[0]);
+                    const float gi1 = p_add(ps[1], pc[1]);
+                    const float gi2 = p_add(ps[2], pc[2]);
                     h3r = p_gru(gi0, gi1, gi2, g3r, g3z, g3n, h3r);
                     x3 = p_add(x2v, h3r);
                 }
@@ -494,12 +545,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     pub(QX3, x3, seq);
                     pub(QH3, h3r, seq);
                 }
+                if (cell) {
+                    float ps[3];
+                    psums(I3(), PB_H1, 3, 0, ps);
+                    g1r = p_add(ps[0], cb[cul]);
+                    g1z = p_add(ps[1], cb[16 + cul]);
+                    g1n = p_add(ps[2], cb[32 + cul]);
+                }
             }
+            RS(4);
             // ---- B3: h3 of every B slot -> W_hh3 h3 (next step's gh3; A runs GRU4) ----------
             fail |= !q_poll(xr, o_cons, q_slot(QH3, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(9), (unsigned)t);
             prod(I3(), 6, cc, PB_H3);
+            RS(5);
             // ---- B4: x4 -> fc1 -> y1 --------------------------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QX4, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(10), (unsigned)t);
+            RS(6);
             prod(I1(), 9, cc, PB_F1);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
@@ -507,32 +568,47 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             {
                 float y = 0.f;
                 if (cell) {
-                    g3r = p_add(psum(PB_H3, 3, 0), cb[48 + cul]);
-                    g3z = p_add(psum(PB_H3, 3, 1), cb[64 + cul]);
-                    g3n = p_add(psum(PB_H3, 3, 2), cb[80 + cul]);
-                    y = p_add(psum(PB_F1, 1, 0), pc[3]);
+                    float ps[3];
+                    psums(I1(), PB_F1, 1, 0, ps);
+                    y = p_add(ps[0], pc[3]);
                 }
                 if (v < 4) pub(QY1, y, seq);
+                if (cell) {
+                    float ps[3];
+                    psums(I3(), PB_H3, 3, 0, ps);
+                    g3r = p_add(ps[0], cb[48 + cul]);
+                    g3z = p_add(ps[1], cb[64 + cul]);
+                    g3n = p_add(ps[2], cb[80 + cul]);
+                }
             }
+            RS(7);
             // ---- B5: y2 -> fc3 -> y3 --------------------------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QY2, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(11), (unsigned)t);
+            RS(8);
             prod(I1(), 10, cc, PB_F3);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
             if (lds[QL_FAIL] != 0.f) return;
             {
                 float y = 0.f;
-                if (cell) y = p_add(psum(PB_F3, 1, 0), pc[4]);
+                if (cell) {
+                    float ps[1];
+                    psums(I1(), PB_F3, 1, 0, ps);
+                    y = p_add(ps[0], pc[4]);
+                }
                 if (v < 4) pub(QY3, y, seq);
             }
+            RS(9);
             // ---- B6: y4 -> fc5 -> per-slot candidates ---------------------------------------
             fail |= !q_poll(xr, o_cons, q_slot(QY4, seq), bvalid, o_own_none, cc, ov, a.ctl, wh(12), (unsigned)t);
+            RS(10);
             if (ntc == 4)
                 prod(std::integral_constant<int, 4>(), 11, cc, PB_F5);
             else
                 prod(std::integral_constant<int, 2>(), 11, cc, PB_F5);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
+            RS(11);
             if (lds[QL_FAIL] != 0.f) return;
             if (v < 4) {
                 const unsigned want = seq & kTagSeqMask;
@@ -542,12 +618,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     float val = -INFINITY;
                     int cls = a.cpw * s + cul;
                     if (cell) {
+                        float ps[4];
+                        if (ntc == 4)
+                            psums(I4(), PB_F5, 4, 0, ps);
+                        else
+                            psums(I2(), PB_F5, 2, 0, ps);
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             if (j >= ntc) break;
                             const int c = a.cpw * s + 16 * j + cul;
                             if (c < a.n_classes) {
-                                const float lg = p_add(psum(PB_F5, ntc, j), cb[96 + 16 * j + cul]);
+                                const float lg = p_add(ps[j], cb[96 + 16 * j + cul]);
                                 p_dbg_logit<DBG>(a.dbg, t, crow, c, a.B, a.n_classes, lg);
                                 const float vj = p_add(lg, pn[j]);
                                 if (vj > val) {
@@ -562,6 +643,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                         __builtin_amdgcn_raw_buffer_store_b64(
                             (u2v){__float_as_uint(val), (want << 11) | (unsigned)cls}, xr, q_cand(cn, s), QX_D * 4, 0);
                 }
+                RS(12);
                 // ---- B7: sample of step t (lanes cul < 8 poll slots 2 cul, 2 cul + 1 of row cn)
                 float x;
                 {
@@ -603,6 +685,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     }
                 }
                 if (fail) lds[QL_FAIL] = 1.f;  // seen by every wave after the next barrier
+                RS(13);
                 // ---- GRU1 of step t + 1 for the slot's units -> x1, h1 ------------------------
                 //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
                 float x1 = 0.f;
@@ -612,6 +695,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                 }
                 pub(QX1, x1, seq + 1u);
                 pub(QH1, h1r, seq + 1u);
+                RS(14);
             }
             if (s == 0 && tid == 0) {
                 if (g == 0) p_progress(a.progress, a.prog_base, t);
@@ -620,6 +704,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         }
     }
 #undef QW
+#undef RS
 }
 
 // launch-side helpers --------------------------------------------------------------------

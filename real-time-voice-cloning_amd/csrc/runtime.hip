@@ -1774,6 +1774,33 @@ void persist_phase_report(wrnn_handle* h, int t) {
     }
 }
 
+// Phase stamps of the runtimeracer wide kernel (kernels_persist_wide_rr.hip RS): wave 0 of
+// slot 0 (half A) and slot 16 (half B) of every group, us from A's step start, median over groups.
+void persist_wide_rr_phase_report(wrnn_handle* h, int t) {
+    std::vector<uint32_t> ph((size_t)kPG * kPM * kPPhases);
+    if (hipMemcpy(ph.data(), h->pws.phases.p, ph.size() * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) return;
+    static const char* na[] = {"top", "x1 poll", "W_ih2 x1", "x2 pub", "h2 poll", "W_hh2 h2", "x3 poll",
+                               "x4 pub", "W_hh4 h4", "y1 poll", "y2 pub", "y3 poll", "y4 pub", "ring"};
+    static const char* nb[] = {"top", "h1 poll", "W_hh1 h1", "x2 poll", "x3 pub", "W_hh3 h3", "x4 poll",
+                               "y1 pub", "y2 poll", "y3 pub", "y4 poll", "fc5", "cand pub", "sample", "x1 pub"};
+    std::fprintf(stderr, "[wrnn persist-wide-rr phases] step %d: slot 0 (A) / slot 16 (B), us from A's step start, median over groups\n", t);
+    for (int half = 0; half < 2; ++half) {
+        const int n = half ? 15 : 14;
+        for (int i = 0; i < n; ++i) {
+            std::vector<double> d;
+            for (int g = 0; g < kPG; ++g) {
+                const uint32_t t0 = ph[(size_t)(g * kPM + 0) * kPPhases];
+                const uint32_t v = ph[(size_t)(g * kPM + 16 * half) * kPPhases + i];
+                if (t0 && v) d.push_back(((long long)v - (long long)t0) * 0.01);
+            }
+            if (d.empty()) continue;
+            std::sort(d.begin(), d.end());
+            std::fprintf(stderr, "  %s %-9s med %6.2f max %6.2f\n", half ? "B" : "A", half ? nb[i] : na[i],
+                         d[d.size() / 2], d.back());
+        }
+    }
+}
+
 // PERSIST engine: P1 for all steps (one MFMA GEMM), Gumbel noise (RAW), step-0 state, then
 // the persistent recurrence in chunks (one chunk per call unless a progress callback wants
 // reports; every 1000 steps then).
@@ -1986,6 +2013,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         ar.k0 = k0;
         ar.k1 = k1;
     }
+    ar.phases = a.phases;
+    ar.phase_t = a.phase_t;
     if (cb && !h->prog_host) {  // progress word + abort word (kAbortWord), two cache lines
         HIPC(hipHostMalloc((void**)&h->prog_host, 128, hipHostMallocMapped | hipHostMallocCoherent));
         HIPC(hipHostGetDevicePointer((void**)&h->prog_dev, h->prog_host, 0));
@@ -2138,7 +2167,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         fail(WRNN_ERR_HIP, msg);
         return kPersistFallback;
     }
-    if (a.phase_t >= 0) persist_phase_report(h, a.phase_t);
+    if (a.phase_t >= 0) {
+        bool rr_wide = false;
+        for (const auto& L : h->p_plan) rr_wide |= L.wide && rr;
+        if (rr_wide) persist_wide_rr_phase_report(h, a.phase_t);
+        else persist_phase_report(h, a.phase_t);
+    }
     // algorithmic traffic per step: recurrent weights once + per row-step
     // conditioning (mel 80 + aux 128 floats) and the label
     // (every tensor of the step: I, rnn*, fc*; MACs: their weight matrices)

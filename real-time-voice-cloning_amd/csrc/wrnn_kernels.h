@@ -310,6 +310,8 @@ struct PersistRRArgs {
     const float* p1taps;
     int p1split;
     uint32_t k0, k1;
+    uint32_t* phases;       // optional: [256][kPPhases] stamps of step phase_t (wide: slots 0, 16)
+    int phase_t;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);

@@ -34,6 +34,17 @@ if [[ ,$S, == *,abrr,* ]]; then
     grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*' $O/abrr_$n.log | tr '\n' ' '; echo
   done
 fi
+if [[ ,$S, == *,abps,* ]]; then
+  # rr wide kernel: serialized vs batched partial-sum reads (exp/lib_ps0 vs exp/lib_ps1)
+  i=0
+  for lib in exp/lib_ps0.so exp/lib_ps1.so exp/lib_ps0.so exp/lib_ps1.so; do
+    i=$((i + 1))
+    n=$(basename $lib .so)_$i
+    run abps_$n 300 env WRNN_LIB=$PWD/$lib python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
+    grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*' $O/abps_$n.log | tr '\n' ' '; echo
+  done
+  run phase_ps1 300 env WRNN_LIB=$PWD/exp/lib_ps1.so WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
+fi
 [[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 [[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 exit 0
