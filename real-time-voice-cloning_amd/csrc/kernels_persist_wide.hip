@@ -288,6 +288,27 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                                                    wide::slot_base(hb, s + 1u), 0);
         }
     };
+    // a cell's sums of the 8 waves' partials of tiles 0 .. K - 1 of the NT-tile buffer at P
+    // (fixed order v = 0 .. 7), every LDS read issued before the first add: at this kernel's
+    // register pressure the scheduler otherwise waits on the reads pair by pair
+    auto psums = [&](auto kc, int P, int NT, float* out) {
+        constexpr int K = decltype(kc)::value;
+        float p[K][8];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int vv = 0; vv < 8; ++vv) p[k][vv] = lds[P + ((vv * NT + k) * 16 + cn) * 16 + wsw(cn, cul)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float s = 0.f;
+#pragma unroll
+            for (int vv = 0; vv < 8; ++vv) s += p[k][vv];
+            out[k] = s;
+        }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I3 = std::integral_constant<int, 3>;
     const rsrc_t fcr = mk_rsrc(a.fcond);
     const rsrc_t rr = mk_rsrc(a.wring + (size_t)g * WR_GROUP);  // this group's operand ring
     // per-step operands of the cell (L2-resident: the per-frame tables and the ring), loaded
@@ -440,13 +461,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             float x2 = 0.f;
             if (cell) {
                 float gi[3];
+                psums(I3(), WL_PA, 3, gi);
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PA + ((vv * 3 + j) * 16 + cn) * 16 + wsw(cn, cul)];
-                    gi[j] = p_add(s, pc[j]);
-                }
+                for (int j = 0; j < 3; ++j) gi[j] = p_add(gi[j], pc[j]);
                 h2r = p_gru(gi[0], gi[1], gi[2], g2r, g2z, g2n, h2r);
                 x2 = p_add(x1c, h2r);
             }
@@ -497,9 +514,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (lo) {
             float y = 0.f;
             if (cell) {
-                float s = 0.f;
-#pragma unroll
-                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
+                float s;
+                psums(I1(), WL_PS, 1, &s);
                 y = p_add(s, pc[3]);
                 y = y > 0.f ? y : 0.f;
             }
@@ -551,9 +567,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (lo) {  // fc2 epilogue: y2 = relu(fc2 y1 + fc2[:, 512:] a4 + b) -> publish
             float y = 0.f;
             if (cell) {
-                float s = 0.f;
-#pragma unroll
-                for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
+                float s;
+                psums(I1(), WL_PS, 1, &s);
                 y = p_add(s, pc[4]);
                 y = y > 0.f ? y : 0.f;
             }
@@ -584,9 +599,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 float val = -INFINITY;
                 int cls = cu;
                 if (cell && cu < a.n_classes) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int vv = 0; vv < 8; ++vv) s += lds[WL_PS + (vv * 16 + cn) * 16 + wsw(cn, cul)];
+                    float s;
+                    psums(I1(), WL_PS, 1, &s);
                     const float lg = p_add(s, lds[WL_BIAS + 96 + cul]);
                     p_dbg_logit<DBG>(a.dbg, t, crow, cu, a.B, a.n_classes, lg);
                     val = p_add(lg, pg);
@@ -603,14 +617,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // this wave reaches both only after these reads have completed.
             if (cell) {
                 float gs[6];
+                psums(I3(), WL_PH, 3, gs);
+                psums(I3(), WL_PA, 3, gs + 3);
 #pragma unroll
-                for (int j = 0; j < 6; ++j) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int vv = 0; vv < 8; ++vv)
-                        s += lds[(j < 3 ? WL_PH : WL_PA) + ((vv * 3 + j % 3) * 16 + cn) * 16 + wsw(cn, cul)];
-                    gs[j] = p_add(s, lds[WL_BIAS + 16 * j + cul]);
-                }
+                for (int j = 0; j < 6; ++j) gs[j] = p_add(gs[j], lds[WL_BIAS + 16 * j + cul]);
                 g1r = gs[0];
                 g1z = gs[1];
                 g1n = gs[2];

@@ -45,6 +45,18 @@ if [[ ,$S, == *,abps,* ]]; then
   done
   run phase_ps1 300 env WRNN_LIB=$PWD/exp/lib_ps1.so WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 fi
+[[ ,$S, == *,widetests,* ]] && run widetests 500 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_gpu_wide.py tests/test_gpu_fullsize.py -k "wide or c4"
+if [[ ,$S, == *,abfw,* ]]; then
+  # fatchord wide kernel: pairwise vs batched partial-sum reads (exp/lib_fw0 vs exp/lib_fw1), C4
+  i=0
+  for lib in exp/lib_fw0.so exp/lib_fw1.so exp/lib_fw0.so exp/lib_fw1.so; do
+    i=$((i + 1))
+    n=$(basename $lib .so)_$i
+    run abfw_$n 300 env WRNN_LIB=$PWD/$lib python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
+    grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*\|"stages_us": {[^}]*}' $O/abfw_$n.log | tr '\n' ' '; echo
+  done
+  run phase_fw1 300 env WRNN_LIB=$PWD/exp/lib_fw1.so WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0 --utts-per-gpu 8
+fi
 [[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 [[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 exit 0
