@@ -2,7 +2,7 @@
 # Round-4 measurement pass on one MI355X box: every step under its own time limit, stops at the
 # first crash / timeout. Outputs under gpurun_out/r04/<TAG>/ (copied to profiles/r04/<TAG>/ after).
 #   tests    : the whole -m gpu suite            smoke : __graft_entry__.smoke()
-#   pmc      : FETCH_SIZE / WRITE_SIZE / SQ passes of the dominant kernels (C2, C4), each its own
+#   pmc      : FETCH_SIZE / WRITE_SIZE / SQ passes of the dominant kernels (C2, C4, rr), each its own
 #              rocprofv3 run; folded on the box into gpurun_out/r04/<TAG>/pmc_traffic.json with
 #              this library's build id (bench lines then name counters of the binary they time)
 #   bench    : default line (C2, CPU baseline, parity, logit gate), counters from the pass above
@@ -34,9 +34,10 @@ if [[ ,$S, == *,pmc,* ]]; then
   python -c "import sys; sys.path[:0]=['.', 'real-time-voice-cloning_amd']; import bench; print(bench.lib_build_id())" > $P/lib_build
   B="/usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 --no-timing"
   SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-  for m in c2 c4; do
+  for m in c2 c4 rr; do
     A=""; K="k_persist<"
     [ $m = c4 ] && A="--utts-per-gpu 8" && K="k_persist|k_gemm"
+    [ $m = rr ] && A="$RR" && K="k_persist_wide_rr"
     run ${m}_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_fetch" -o run --output-format csv -- $B $A
     run ${m}_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_write" -o run --output-format csv -- $B $A
     run ${m}_sq 240 rocprofv3 --pmc $SQ --kernel-include-regex "$K" -d "$PWD/$P/${m}_sq" -o run --output-format csv -- $B $A
