@@ -57,6 +57,26 @@ if [[ ,$S, == *,abfw,* ]]; then
   done
   run phase_fw1 300 env WRNN_LIB=$PWD/exp/lib_fw1.so WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0 --utts-per-gpu 8
 fi
+if [[ ,$S, == *,wsrc,* ]]; then
+  # where do the wide kernel's HBM writes come from? WRITE_SIZE of the shipped build against
+  # builds without the ring's noise stores (wnn) / P1 stores (wnp); outputs of those are wrong
+  # (each build copied over the in-tree library of this scratch copy: under WRNN_LIB the
+  # profiler recorded no dispatches)
+  L=real-time-voice-cloning_amd/wavernn_amd/libwavernn_mi355x.so
+  cp $L exp/lib_shipped.so
+  for lib in exp/lib_shipped.so exp/lib_wnn.so exp/lib_wnp.so; do
+    n=$(basename $lib .so)
+    cp $lib $L
+    run wsrc_$n 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_persist_wide -d "$PWD/$O/wsrc_$n" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-timing --utts-per-gpu 8
+    python3 -c "
+import csv,collections,sys
+d=collections.defaultdict(float); n=set()
+for r in csv.DictReader(open('$O/wsrc_$n/run_counter_collection.csv')):
+    if 'k_persist_wide' in r['Kernel_Name']: d[r['Counter_Name']]+=float(r['Counter_Value']); n.add(r['Dispatch_Id'])
+print('$n', {k: v*1024/1e9/len(n) for k,v in d.items()}, 'GB per launch,', len(n), 'launches')" | tee -a $O/steps.log
+  done
+  cp exp/lib_shipped.so $L
+fi
 [[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 [[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 exit 0
