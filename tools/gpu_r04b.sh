@@ -64,16 +64,23 @@ if [[ ,$S, == *,wsrc,* ]]; then
   # profiler recorded no dispatches)
   L=real-time-voice-cloning_amd/wavernn_amd/libwavernn_mi355x.so
   cp $L exp/lib_shipped.so
-  for lib in exp/lib_shipped.so exp/lib_wnn.so exp/lib_wnp.so; do
+  for lib in exp/lib_shipped.so ${WSRC_LIBS:-exp/lib_wnn.so exp/lib_wnp.so}; do
     n=$(basename $lib .so)
     cp $lib $L
-    run wsrc_$n 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_persist_wide -d "$PWD/$O/wsrc_$n" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-timing --utts-per-gpu 8
+    run wsrc_$n 240 env WRNN_WIDE_ALLOW_SCRATCH=1 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_persist_wide -d "$PWD/$O/wsrc_$n" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --no-timing --utts-per-gpu 8
     python3 -c "
 import csv,collections,sys
 d=collections.defaultdict(float); n=set()
 for r in csv.DictReader(open('$O/wsrc_$n/run_counter_collection.csv')):
     if 'k_persist_wide' in r['Kernel_Name']: d[r['Counter_Name']]+=float(r['Counter_Value']); n.add(r['Dispatch_Id'])
 print('$n', {k: v*1024/1e9/len(n) for k,v in d.items()}, 'GB per launch,', len(n), 'launches')" | tee -a $O/steps.log
+  done
+  # and the C4 timing of each (in-place copies again)
+  for lib in exp/lib_shipped.so ${WSRC_LIBS:-} exp/lib_shipped.so ${WSRC_LIBS:-}; do
+    n=$(basename $lib .so)
+    cp $lib $L
+    run wsab_$n 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
+    grep -o '"value": [0-9.]*\|"stages_us": {[^}]*}' $O/wsab_$n.log | tr '\n' ' ' | tee -a $O/steps.log; echo | tee -a $O/steps.log
   done
   cp exp/lib_shipped.so $L
 fi
