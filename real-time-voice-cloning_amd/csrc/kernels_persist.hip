@@ -397,7 +397,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         PSTAMP(2);
         // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
         auto mv1 = [&](float bias) {
@@ -510,7 +509,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             XSTAMP(31);
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         PSTAMP(4);
         // ================= stage C: fc2 (waves 0-3, critical) ================================
         if (gate_a) {
@@ -540,7 +538,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             p1_store(t + 2);
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         PSTAMP(6);
         float pG[NR][3];  // GRU1 operands, loaded once this wave's fc3 work is issued
         auto gru1_loads = [&]() {
@@ -781,6 +778,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             }
         }
         __syncthreads();
+        // The step's one failure check: a wave whose poll gave up (timeout, or PC_ERR raised by
+        // another slot) finishes the step on whatever its buffers hold, and every other poll
+        // of the step ends within 256 spins of PC_ERR, so all waves reach this barrier. (A check
+        // after every hop's barrier cost an LDS round trip each, in front of the stage's own
+        // LDS reads.)
         if (lds[L_FAIL] != 0.f) return;
         PSTAMP(9);
         // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         pgum = pgn;
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
-            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen after hop A's barrier
+            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen after the next sample
         }
         __syncthreads();
         PSTAMP(10);

@@ -84,6 +84,17 @@ print('$n', {k: v*1024/1e9/len(n) for k,v in d.items()}, 'GB per launch,', len(n
   done
   cp exp/lib_shipped.so $L
 fi
+if [[ ,$S, == *,abgen,* ]]; then
+  # generic A/B: AB_LIBS (space-separated builds), alternated twice, bench args AB_ARGS
+  i=0
+  for lib in ${AB_LIBS} ${AB_LIBS}; do
+    i=$((i + 1))
+    n=$(basename $lib .so)_$i
+    run abgen_$n 300 env WRNN_LIB=$PWD/$lib python bench.py --steps 5 --warmup 2 --cpu-seconds 0 ${AB_ARGS:-}
+    grep -o '"value": [0-9.]*\|"us_per_step": [0-9.]*\|"stages_us": {[^}]*}' $O/abgen_$n.log | tr '\n' ' ' | tee -a $O/steps.log; echo | tee -a $O/steps.log
+  done
+fi
+[[ ,$S, == *,c2tests,* ]] && run c2tests 600 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_callback.py tests/test_gpu_logits.py
 [[ ,$S, == *,rrbench,* ]] && run rrbench 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 [[ ,$S, == *,rrbench0,* ]] && run rrbench0 600 env WRNN_PERSIST_WIDE=0 python bench.py --steps 1 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8
 exit 0
