@@ -229,7 +229,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
         }
         if (!poll_rows<NR, GF>(xr, QX_Y * 4, seq, lds + L_Y, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 2: fc3 -> candidates; gh1 of this step into LDS ===========
         {
             float s0 = 0.f;
@@ -259,7 +258,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             // producer overwrites them only after every candidate of this step is out)
             if (!poll_rows<NR, 3 * GH>(xr, QX_GH * 4, seq, lds + L_GH, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
             __syncthreads();
-            if (lds[L_FAIL] != 0.f) return;
             if (wave == 0) {
                 if (MODE == 0) {
                     const unsigned tag_hi = (seq & kTagSeqMask) << 11;
@@ -414,6 +412,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             }
         }
         __syncthreads();
+        // the step's one failure check (as kernels_persist.hip): a wave whose poll gave up
+        // finishes the step, every other poll of it ends within a few spins of PC_ERR
         if (lds[L_FAIL] != 0.f) return;
         // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
         // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
-            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next hop's check
+            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next step's check
         }
         __syncthreads();
     }

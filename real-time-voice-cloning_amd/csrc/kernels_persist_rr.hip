@@ -355,7 +355,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             if (!poll_hop<NR, 2>(xr, sg(0), seq, lds + L_XB, lds + L_H2, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 2: q0 GRU3 | q2 gh2 (next step) ============================
         if (q == 0) {
             __builtin_amdgcn_s_setprio(2);
@@ -392,7 +391,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             if (!poll_hop<NR, 2>(xr, sg(1), seq, lds + L_XA, lds + L_H3, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 3: q1 GRU4 | q2 gh3 (next step) ============================
         if (q == 1) {
             __builtin_amdgcn_s_setprio(2);
@@ -434,7 +432,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             if (!poll_hop<NR, 2>(xr, sg(2), seq, lds + L_XB, lds + L_H4, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // GRU1 operands of the end of this step: every slot's gh1 is in L2 (drained before its
         // x4/h4 publish, all of which this workgroup has seen)
         float pG[NRH][3];
@@ -492,7 +489,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         if (!poll_hop<NR, 1>(xr, sf(0), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 5: q2 fc2 (relu) ===========================================
         if (q == 2) {
             __builtin_amdgcn_s_setprio(2);
@@ -510,7 +506,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         if (!poll_hop<NR, 1>(xr, sf(1), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 6: q1 fc3 ==================================================
         if (q == 1) {
             __builtin_amdgcn_s_setprio(2);
@@ -520,7 +515,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         if (!poll_hop<NR, 1>(xr, sf(2), seq, lds + L_XA, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 7: q0 fc4 (relu) ===========================================
         if (q == 0) {
             __builtin_amdgcn_s_setprio(2);
@@ -533,7 +527,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         if (!poll_hop<NR, 1>(xr, sf(3), seq, lds + L_XB, nullptr, sink, a.ctl, tid)) lds[L_FAIL] = 1.f;
         __syncthreads();
-        if (lds[L_FAIL] != 0.f) return;
         // ================= stage 8: fc5 -> per-slot candidates (RAW) / logits (MOL) =========
         {
             float s0 = 0.f;
@@ -697,6 +690,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             }
         }
         __syncthreads();
+        // the step's one failure check (as kernels_persist.hip): a wave whose poll gave up
+        // finishes the step, every other poll of it ends within a few spins of PC_ERR
         if (lds[L_FAIL] != 0.f) return;
         // (at the last step this GRU1 runs on clamped inputs and its result goes unused)
         // ================= GRU1 of step t+1 for all 256 units (redundant) ===================
@@ -714,7 +709,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
-            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next hop's check
+            if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next step's check
         }
         __syncthreads();
     }

@@ -452,6 +452,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(2);
+        // The step's one failure check: a wave whose poll gave up (timeout, or PC_ERR raised by
+        // another slot) finishes the step on whatever its registers hold; every other poll of
+        // the step ends within 64 spins of PC_ERR, so all waves come back here. (A check after
+        // every stage barrier cost an LDS round trip each in front of the epilogue's reads.)
         if (lds[WL_FAIL] != 0.f) return;
         // h1 (published with x1, read above) loads now: in flight over the GRU2 epilogue, so the
         // off-path W_hh1 h1 starts without an L2 round trip
@@ -509,7 +513,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(5);
-        if (lds[WL_FAIL] != 0.f) return;
         // fc1 epilogue (waves 0-3): y1 = relu(fc1 x2 + fc1[:, 512:] a3 + b) -> publish
         if (lo) {
             float y = 0.f;
@@ -563,7 +566,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(7);
-        if (lds[WL_FAIL] != 0.f) return;
         if (lo) {  // fc2 epilogue: y2 = relu(fc2 y1 + fc2[:, 512:] a4 + b) -> publish
             float y = 0.f;
             if (cell) {
@@ -590,7 +592,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
         WSTAMP(9);
-        if (lds[WL_FAIL] != 0.f) return;
         if (lo) {
             const unsigned tag_hi = (seq & kTagSeqMask) << 11;
             // fc3 epilogue: candidate argmax_k (l_k + g_k) over the slot's 16 classes per row
@@ -675,7 +676,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     bst(x, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
                 }
             }
-            if (fail) lds[WL_FAIL] = 1.f;  // seen by every wave after the next barrier
+            if (fail) lds[WL_FAIL] = 1.f;  // seen by every wave at the next stage-A check
             WSTAMP(10);
             // ============= GRU1 of step t + 1 for the slot's units -> publish x1, h1 ========
             //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
@@ -698,7 +699,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
-            if (p_abort(a.ctl, a.progress, t)) lds[WL_FAIL] = 1.f;  // seen after the next barrier
+            if (p_abort(a.ctl, a.progress, t)) lds[WL_FAIL] = 1.f;  // seen at the next stage-A check
         }
         WSTAMP(11);
     }

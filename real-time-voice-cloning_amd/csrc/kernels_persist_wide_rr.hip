@@ -380,7 +380,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             prod(I3(), 6, cc, PA_G4);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
-            if (lds[QL_FAIL] != 0.f) return;
             {
                 float x4 = 0.f;
                 if (cell) {
@@ -415,7 +414,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             prod(I1(), 12, cc, PA_F2);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
-            if (lds[QL_FAIL] != 0.f) return;
             {
                 float y = 0.f;
                 if (cell) {
@@ -440,7 +438,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             prod(I1(), 13, cc, PA_F4);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
-            if (lds[QL_FAIL] != 0.f) return;
             {
                 float y = 0.f;
                 if (cell) {
@@ -564,7 +561,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             prod(I1(), 9, cc, PB_F1);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
-            if (lds[QL_FAIL] != 0.f) return;
             {
                 float y = 0.f;
                 if (cell) {
@@ -588,7 +584,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             prod(I1(), 10, cc, PB_F3);
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
-            if (lds[QL_FAIL] != 0.f) return;
             {
                 float y = 0.f;
                 if (cell) {
@@ -609,7 +604,6 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             if (fail) lds[QL_FAIL] = 1.f;
             qbar();
             RS(11);
-            if (lds[QL_FAIL] != 0.f) return;
             if (v < 4) {
                 const unsigned want = seq & kTagSeqMask;
                 {
@@ -684,7 +678,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                         bst(x, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
                     }
                 }
-                if (fail) lds[QL_FAIL] = 1.f;  // seen by every wave after the next barrier
+                if (fail) lds[QL_FAIL] = 1.f;  // seen by every wave at the half's next check
                 RS(13);
                 // ---- GRU1 of step t + 1 for the slot's units -> x1, h1 ------------------------
                 //   gi = W_ih1 (cI + w0 x) + b_ih1 = P1 + v x ; x1 = (cI + w0 x) + h1
@@ -699,7 +693,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             }
             if (s == 0 && tid == 0) {
                 if (g == 0) p_progress(a.progress, a.prog_base, t);
-                if (p_abort(a.ctl, a.progress, t)) lds[QL_FAIL] = 1.f;  // seen after the next barrier
+                if (p_abort(a.ctl, a.progress, t)) lds[QL_FAIL] = 1.f;  // seen at the half's next check
             }
         }
     }
