@@ -53,6 +53,13 @@ def parse():
     return ap.parse_args()
 
 
+def workload_of(utts, frames, model, wname, target, overlap):
+    """The line's config.workload string; also the key under which tools/pmc_traffic.py files
+    the counters of a workload (with the kernel name)."""
+    return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
+            f'batched folds target={target} overlap={overlap}')
+
+
 def _pmc_traffic(kernel, workload):
     # WRNN_PMC_TRAFFIC: a table folded on the box from this build's own counter passes
     # (tools/measure_r04.sh), so the line's counters come from the binary it times
@@ -345,8 +352,7 @@ def main():
 
     wname = ('MOL' if hp.mode == 'MOL' else 'RAW (Beta)' if args.model == 'geneing-wavernn' and hp.mode == 'RAW'
              else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else ''))
-    workload = (f'{U}x{args.frames}-frame mel per GPU, {args.model} {wname}, '
-                f'batched folds target={args.target} overlap={args.overlap}')
+    workload = workload_of(U, args.frames, args.model, wname, args.target, args.overlap)
     roof = None
     info = model.stage_info() if not args.no_timing else []
     rows_per_gpu = U * model.fold_shape(args.frames, True, args.target, args.overlap)[0]
