@@ -2,7 +2,7 @@
 record the kernels' logits (teacher-forced: the labels agree up to that step) at the first
 differing (row, step) and compare them with the oracle's: the logit error against the decision's
 top-1 / top-2 gap. Usage (GPU box):
-  python tools/near_tie_gpu.py <default|peaked> <weight_seed> <noise_seed> <utts> <utterance> <row> <step>
+  python tools/near_tie_gpu.py <default|peaked> <weight_seed> <noise_seed> <utts> <utterance> <row> <step> [fatchord|runtimeracer]
 (mel seed of utterance u = 200 + case + 1000 u as in tools/parity_sweep.py; pass the sweep's
 mel_seed of utterance 0 minus 200 as the case through weight_seed - 100)."""
 import json
@@ -23,25 +23,28 @@ from wavernn_amd.model import WaveRNN
 from wavernn_amd.synth import synth_mel, synth_state_dict
 
 kind, wseed, nseed, utts, u, row, step = sys.argv[1], *map(int, sys.argv[2:8])
+topo = sys.argv[8] if len(sys.argv) > 8 else 'fatchord'
+MT = topo + '-wavernn'
+BITS, TARGET, OVERLAP = (10, 6000, 1000) if topo == 'runtimeracer' else (9, 11000, 550)
 case = wseed - 100
 stats = dict(gru_scale=3.0, fc_scale=2.0, logit_scale=16.0) if kind == 'peaked' else {}
 torch.set_num_threads(16)
-hp = hparams_for('fatchord-wavernn').copy(bits=9, mode='RAW')
-sd = synth_state_dict(hp, 'fatchord-wavernn', seed=wseed, **stats)
+hp = hparams_for(MT).copy(bits=BITS, mode='RAW')
+sd = synth_state_dict(hp, MT, seed=wseed, **stats)
 m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
             hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
-            mode='RAW', model_type='fatchord-wavernn', device=0)
+            mode='RAW', model_type=MT, device=0)
 m.load_state_dict(sd)
 m.set_seed(nseed)
 mels = [synth_mel(1000, 200 + case + 1000 * k) for k in range(utts)]
 devs = [torch.from_numpy((x / sp.max_abs_value).astype(np.float32)).cuda() for x in mels]
 m.set_debug_steps([step])
-out, roff, S = m.generate_batch_device(devs, True, 11000, 550)
+out, roff, S = m.generate_batch_device(devs, True, TARGET, OVERLAP)
 lab = out.cpu().numpy()[roff[u]:roff[u + 1]]
 g_log = m.debug_logits(step, [roff[u] + row])[0].astype(np.float64)
 sdt = {k: torch.from_numpy(np.asarray(v)) if not torch.is_tensor(v) else v for k, v in sd.items()}
-o = OracleWaveRNN(sdt, hp, 'fatchord-wavernn').generate(
-    torch.from_numpy((mels[u] / sp.max_abs_value)[None].astype(np.float32)), True, 11000, 550,
+o = OracleWaveRNN(sdt, hp, MT).generate(
+    torch.from_numpy((mels[u] / sp.max_abs_value)[None].astype(np.float32)), True, TARGET, OVERLAP,
     hp.mu_law, True, seed=nseed, stream=u, max_steps=step + 1, record_logits=[step], post=False)
 o_log = o['logits'][step][row].astype(np.float64)
 q = philox.raw_exp_noise(nseed, u, [step], np.arange(lab.shape[0]), 2 ** hp.bits)[0][row]
@@ -55,7 +58,7 @@ def decide(lg):
 
 
 (gk, ggap), (ok, ogap) = decide(g_log), decide(o_log)
-print(json.dumps({'kind': kind, 'case': case, 'utts': utts, 'utterance': u, 'row': row, 'step': step,
+print(json.dumps({'model': MT, 'kind': kind, 'case': case, 'utts': utts, 'utterance': u, 'row': row, 'step': step,
                   'labels_equal_before_step': bool(np.array_equal(lab[:, :step], o['labels'][:, :step])),
                   'gpu_label': int(lab[row, step]), 'oracle_label': int(o['labels'][row, step]),
                   'oracle_top2': ok, 'oracle_gap': ogap, 'gpu_top2': gk, 'gpu_gap': ggap,
