@@ -99,12 +99,15 @@ def _cpu_model():
 # handoff-1to1: 0.8 us idle for an 8-byte granule) plus the critical-path products of one
 # workgroup at the fp32 vector peak (64 FLOP/clk/SIMD x 4 SIMDs x 2.4 GHz).
 HANDOFF_US = 0.8
+# the same hand-off with the endpoint CUs busy (the guide's row: 2 streaming waves -> 1.2 us for
+# an 8-byte granule): the loaded floor, so the headroom claim is bounded from both sides
+HANDOFF_LOADED_US = 1.2
 CU_FP32_FLOP_PER_US = 64 * 4 * 2400.0
 PERSIST_HOPS = {'fatchord-wavernn': 4, 'runtimeracer-wavernn': 8, 'geneing-wavernn': 2}
 
 
 # MACs per row-step of the recurrent weight matrices
-def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False):
+def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False, handoff_us=HANDOFF_US):
     """Lower bound of one persistent step: exchange hops + critical products of one slot.
     Wide launches (kernels_persist_wide.hip) have one more hop (GRU1 is distributed) and run
     the products on 16-column MFMA tiles: 16 rows of work whatever the row count."""
@@ -120,7 +123,7 @@ def latency_floor_us(model_type, hp, rows_per_group, n_classes, wide=False):
         crit = F * H + n_classes * F
     flop = 2.0 * crit * rows_per_group / slots
     hops = PERSIST_HOPS[model_type] + (1 if wide else 0)
-    return hops * HANDOFF_US + flop / CU_FP32_FLOP_PER_US, hops
+    return hops * handoff_us + flop / CU_FP32_FLOP_PER_US, hops
 
 
 def _oracle_run(args, sd, hp, mel, threads, max_steps=None, seed=0, stream=0, **kw):
@@ -388,9 +391,14 @@ def main():
             nr = -(-int(round(rows_l)) // 8)
             floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes,
                                            wide=name == 'persist_wide')
+            floor_l, _ = latency_floor_us(args.model, hp, nr, model.n_classes, wide=name == 'persist_wide',
+                                          handoff_us=HANDOFF_LOADED_US)
             roof['latency_floor_us'] = floor
             roof['latency_frac'] = floor / roof['us_per_step']
-            roof['latency_model'] = (f'{hops} in-group hops x {HANDOFF_US} us (handoff-1to1) + '
+            roof['latency_floor_loaded_us'] = floor_l
+            roof['latency_frac_loaded'] = floor_l / roof['us_per_step']
+            roof['latency_model'] = (f'{hops} in-group hops x {HANDOFF_US} us (handoff-1to1, idle) or '
+                                     f'x {HANDOFF_LOADED_US} us (loaded: endpoint CUs streaming) + '
                                      f'critical products of one slot at the fp32 vector peak, '
                                      f'{nr} rows per XCD group')
         # HBM traffic of the same kernel on the same workload from the committed PMC passes

@@ -222,6 +222,15 @@ int wrnn_post_assemble(const int16_t* labels, int nf, int S, int overlap, const 
 int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row, float alpha,
                     float beta, float* out);
 
+/* Host restatement of the RAW decision every kernel makes (csrc/cand_key.h): for
+ * the n_classes logits of one (step, fold, stream) row, the class argmax_k (l_k + G_k), G_k =
+ * -log q_k of the Philox contract's Exp(1) variate (philox.h gumbel_q_of: float64 logs, fixed
+ * point to 2^-27), l + G formed exactly -- the reference's argmax((softmax(l)/sum)/q) without
+ * fp32 rounding of its own. `margin` (may be NULL) receives the float64 value of the decision's
+ * top-1 minus top-2 l + G (how far it was from a flip). No device needed (tests). */
+int wrnn_debug_decide(uint64_t seed, uint32_t stream, uint32_t step, uint32_t fold, const float* logits,
+                      int n_classes, int* label, double* margin);
+
 /* Host-side exhaustive check of the wide launch's exchange layout (kernels_persist_wide.hip,
  * csrc/wide_layout.h) for a group of `rows_per_group` rows (1..16): returns the number of
  * violations (0 = every producer packet of a hop lands on exactly the consumer packet that

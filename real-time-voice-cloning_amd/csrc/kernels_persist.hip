@@ -23,8 +23,9 @@
 // follow (behind a workgroup barrier): W_hh1 h1 + b -> gh1 (published) in hop A, W_hh2 h2 + b
 // -> gh2 of the next step (kept local) in hops B and C. Redundantly in every workgroup: the
 // sample of step t and GRU1 of step t+1 for all 512 units (so x1/h1 never need an exchange).
-// Sampling: argmax_k (l_k + g_k), g_k = -log q_k with q the RNG contract's Exp(1) variate --
-// the same decision as the reference's argmax((softmax(l)/sum)/q) in exact arithmetic.
+// Sampling: argmax_k (l_k + G_k), G_k = -log q_k with q the RNG contract's Exp(1) variate,
+// G in fixed point to 2^-27 and the sum in float64 (persist_common.h cand_key) -- the
+// reference's argmax((softmax(l)/sum)/q) without the fp32 rounding of round 4's l + g.
 // Every spin is bounded; on a timeout the kernel sets an error code and every group exits.
 #include "wrnn_kernels.h"
 #include "persist_common.h"
@@ -176,10 +177,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     // (waves 0-3: hop C, waves 4-7: hop B) so the publish never waits on them:
     //   pP/pC  P1(tg+1), cI(tg+1) of this thread's GRU1 unit   (end of step tg)
     //   pc*    per-frame conditioning of step te's epilogues  (stages A-C of step te)
-    //   pgn    Gumbel noise of step te, class cls (copied to pgum at the end of step te-1)
+    //   pgn    noise of step te, class cls (copied to pgum at the end of step te-1)
     float pP[NR][3], pC[NR];
-    float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f, pgum = 0.f, pgn = 0.f;
-    // At <= 16 classes per slot waves 4-7 hold no fc3 class: they issue their GRU1 loads
+    float pc0 = 0.f, pc1 = 0.f, pc2 = 0.f, pf2 = 0.f;
+    // pgn / pgum: RAW -- the lane's Gumbel noise in the contract's fixed-point form (k_gumbel,
+    // philox.h gumbel_q_of: G = -log q to 2^-27, as a 32-bit word in a float register);
+    // MOL -- the lane's draw of k_mol_noise
+    float pgum = 0.f, pgn = 0.f;    // At <= 16 classes per slot waves 4-7 hold no fc3 class: they issue their GRU1 loads
     // while waves 0-3 compute fc3 (LDS only) and later poll the candidates; waves 0-3
     // issue theirs after the candidate publish, off the critical path (a wave polls only
     // with no bulk loads in flight: its first poll would wait for all of them).
@@ -606,19 +610,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             } else {
                 fc3();
             }
-            float* red = lds + L_RED;  // [og][r][value, class]
+            // [og][r] (logit, noise word) of (row r, class og's); wave 0 forms the candidate keys
+            // (cand_key) as it reduces them -- the float64 sum in this epilogue, beside the fc3
+            // accumulators, spilled the 4-row variant
+            float* red = lds + L_RED;
             if (kc < NR) {
-                float val = -INFINITY;
+                float l = -INFINITY;
                 if (has_cls) {
-                    const float l = p_add(s0, lds[L_BCLS + og]);
+                    l = p_add(s0, lds[L_BCLS + og]);
                     p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
-                    if (!MOL)
-                        val = p_add(l, pgum);
-                    else  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
+                    if (MOL)  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
                         bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
                 }
-                red[(og * kPNR + kc) * 2] = val;
-                red[(og * kPNR + kc) * 2 + 1] = __int_as_float(cls);
+                *reinterpret_cast<float2*>(red + (og * kPNR + kc) * 2) = make_float2(l, pgum);
             }
             XSTAMP(28);
             __syncthreads();
@@ -626,40 +630,40 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             if (wv_lo) {
             if (wave == 0) {
                 if (!MOL) {
-                    // slot candidate per row, tagged with the step (no flag, no wait)
-                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    // slot candidate per row: the max key, tagged with the step (no flag, no wait)
+                    const unsigned tag = key_tag(seq);
                     int tt = tid;  // (lane offsets recomputed per step: hoisted ones cost registers)
                     asm volatile("" : "+v"(tt));
                     if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
                         const int r = tt >> 4, o = tt & 15;
-                        float bv = -INFINITY;
-                        int bi = 0x7fffffff;
-                        if (r < NR && o < a.cpw) {
-                            bv = red[(o * kPNR + r) * 2];
-                            bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                        uint32_t bh = 0, bl = 0;
+                        if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+                            const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
+                            const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
+                            bh = k.hi;
+                            bl = k.lo;
                         }
-                        row16_argmax(bv, bi);
+                        row16_kmax(bh, bl);
                         const int rr = r;
                         if (r < NR && o == 0)
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64((u2v){bh, bl | tag}, xr,
+                                                                  (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
                     } else {
 #pragma unroll
                         for (int rb = 0; rb < NR; rb += 2) {
                             const int r = rb + (tt >> 5), o = tt & 31;
-                            float bv = -INFINITY;
-                            int bi = 0x7fffffff;
-                            if (r < NR && o < a.cpw) {
-                                bv = red[(o * kPNR + r) * 2];
-                                bi = __float_as_int(red[(o * kPNR + r) * 2 + 1]);
+                            uint32_t bh = 0, bl = 0;
+                            if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+                                const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
+                                const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
+                                bh = k.hi;
+                                bl = k.lo;
                             }
-                            half_argmax(bv, bi);
+                            half_kmax(bh, bl);
                             const int rr = r;
                             if (r < NR && o == 31)
-                                __builtin_amdgcn_raw_buffer_store_b64(
-                                    (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                    (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
+                                __builtin_amdgcn_raw_buffer_store_b64((u2v){bh, bl | tag}, xr,
+                                                                      (unsigned)((w * kPNR + rr) * 2) * 4u, XB_D * 4, 0);
                         }
                     }
                 }
@@ -680,17 +684,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         if (!MOL) {
             if (st >= 0 && st < 32 * NR) {  // half-wave r: lane o polls slot o's candidate of row r
                 const int r = st >> 5, o = st & 31;
-                const unsigned want = seq & kTagSeqMask;
+                const unsigned want = key_tag(seq);
                 const unsigned t0 = p_now();
                 unsigned n = 0;
-                float bv;
-                int bi;
+                uint32_t bh, bl;
                 {
                     const unsigned off = (unsigned)((o * kPNR + r) * 2) * 4u;
                     u2v c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
                     while (true) {  // two polls in flight (see poll_couples)
                         const u2v c1 = __builtin_amdgcn_raw_buffer_load_b64(xr, off, XB_D * 4, kCpNT);
-                        if (__all((c.y >> 11) == want)) break;
+                        if (__all((c.y & kKeyTagMask) == want)) break;
                         c = c1;
                         if ((++n & 255) == 0) {
                             if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0 > kSpinTicks) {
@@ -700,11 +703,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                             }
                         }
                     }
-                    bv = __uint_as_float(c.x);
-                    bi = (int)(c.y & 0x7ffu);
+                    bh = c.x;
+                    bl = c.y;
                 }
-                half_argmax(bv, bi);
+                half_kmax(bh, bl);  // the 32 slots' candidates: argmax over all classes of row r
                 if (o == 31) {
+                    const int bi = key_cls(bl);
                     float xv;
                     {
 #pragma clang fp contract(off)
@@ -850,9 +854,9 @@ hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s) {
 }
 
 // RAW Gumbel noise of every (step, row, class) of rows [r0, r0 + nrows) of the [S][ld][n]
-// buffer: philox.h gumbel_of (wide launches form theirs in-kernel, so a plan with them fills
-// only the register-resident launches' rows)
-__global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int r0, int nrows, int ld, int ng,
+// buffer in the fixed-point form philox.h gumbel_q_of (wide launches form theirs in-kernel, so
+// a plan with them fills only the register-resident launches' rows)
+__global__ __launch_bounds__(256) void k_gumbel(uint4* g, int S, int r0, int nrows, int ld, int ng,
                                                 const RowInfo* rows, uint32_t k0, uint32_t k1) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // (t, r, k4)
     const size_t total = (size_t)S * nrows * ng;
@@ -862,12 +866,7 @@ __global__ __launch_bounds__(256) void k_gumbel(float4* g, int S, int r0, int nr
     const int r = r0 + (int)(tr % nrows), t = (int)(tr / nrows);
     const RowInfo ri = rows[r];
     const U4 o = philox4x32_10((uint32_t)k4, (uint32_t)t, (uint32_t)ri.fold, ri.stream, k0, k1);
-    float4 v;
-    v.x = gumbel_of(o.x);
-    v.y = gumbel_of(o.y);
-    v.z = gumbel_of(o.z);
-    v.w = gumbel_of(o.w);
-    g[((size_t)t * ld + r) * ng + k4] = v;
+    g[((size_t)t * ld + r) * ng + k4] = make_uint4(gumbel_q_of(o.x), gumbel_q_of(o.y), gumbel_q_of(o.z), gumbel_q_of(o.w));
 }
 
 hipError_t launch_gumbel(float* g, int S, int nrows, int n_classes, const RowInfo* rows,
@@ -882,7 +881,7 @@ hipError_t launch_gumbel_rows(float* g, int S, int r0, int nrows, int ld, int n_
     const size_t total = (size_t)S * nrows * ng;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_gumbel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<float4*>(g), S, r0, nrows, ld, ng, rows, k0, k1);
+                       reinterpret_cast<uint4*>(g), S, r0, nrows, ld, ng, rows, k0, k1);
     return hipGetLastError();
 }
 

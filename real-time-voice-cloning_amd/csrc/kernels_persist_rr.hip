@@ -544,50 +544,50 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                     if (kc == r) s0 = tt;
                 }
             }
-            float* red = lds + L_RED;  // [cl][r][value, class]
+            // [cl][r] (logit, noise word): wave 0 forms the candidate keys (cand_key) as it
+            // reduces them; MOL: the logit, published after the barrier below
+            float* red = lds + L_RED;
             if (own) {
-                float val = -INFINITY;
+                float l = -INFINITY;
                 if (has_cls) {
-                    const float l = p_add(s0, bcls);
+                    l = p_add(s0, bcls);
                     p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
-                    // (MOL: the logit itself, published after the barrier below)
-                    val = MOL ? l : p_add(l, pgum);
                 }
-                red[(cl * kRNR + kc) * 2] = val;
-                red[(cl * kRNR + kc) * 2 + 1] = __int_as_float(cls);
+                *reinterpret_cast<float2*>(red + (cl * kRNR + kc) * 2) = make_float2(l, pgum);
             }
             __syncthreads();
             if (wave == 0) {
                 if (!MOL) {
-                    const unsigned tag_hi = (seq & kTagSeqMask) << 11;
+                    // slot candidate per row: the max key, tagged with the step
+                    const unsigned tag = key_tag(seq);
                     if (a.cpw <= 16) {  // DPP row r = lane / 16 reduces the slot's classes of row r
                         const int r = tid >> 4, o = tid & 15;
-                        float bv = -INFINITY;
-                        int bi = 0x7fffffff;
-                        if (r < NR && o < a.cpw) {
-                            bv = red[(o * kRNR + r) * 2];
-                            bi = __float_as_int(red[(o * kRNR + r) * 2 + 1]);
+                        uint32_t bh = 0, bl = 0;
+                        if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+                            const float2 lg = *reinterpret_cast<const float2*>(red + (o * kRNR + r) * 2);
+                            const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
+                            bh = k.hi;
+                            bl = k.lo;
                         }
-                        row16_argmax(bv, bi);
+                        row16_kmax(bh, bl);
                         if (r < NR && o == 0)
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64((u2v){bh, bl | tag}, xr,
+                                                                  (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
                     } else {
 #pragma unroll
                         for (int rb = 0; rb < NR; rb += 2) {
                             const int r = rb + (tid >> 5), o = tid & 31;
-                            float bv = -INFINITY;
-                            int bi = 0x7fffffff;
-                            if (r < NR && o < a.cpw) {
-                                bv = red[(o * kRNR + r) * 2];
-                                bi = __float_as_int(red[(o * kRNR + r) * 2 + 1]);
+                            uint32_t bh = 0, bl = 0;
+                            if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+                                const float2 lg = *reinterpret_cast<const float2*>(red + (o * kRNR + r) * 2);
+                                const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
+                                bh = k.hi;
+                                bl = k.lo;
                             }
-                            half_argmax(bv, bi);
+                            half_kmax(bh, bl);
                             if (r < NR && o == 31)
-                                __builtin_amdgcn_raw_buffer_store_b64(
-                                    (u2v){__float_as_uint(bv), tag_hi | (unsigned)bi}, xr,
-                                    (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
+                                __builtin_amdgcn_raw_buffer_store_b64((u2v){bh, bl | tag}, xr,
+                                                                      (unsigned)((w * kRNR + r) * 2) * 4u, RX_D * 4, 0);
                         }
                     }
                 } else {
@@ -605,13 +605,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             if (tid < 32 * NR) {  // half-wave r: lane o polls slot o's tagged candidate of row r
                 const int r = tid >> 5, o = tid & 31;
                 const unsigned off = (unsigned)((o * kRNR + r) * 2) * 4u;
-                const unsigned want = seq & kTagSeqMask;
+                const unsigned want = key_tag(seq);
                 u2v c;
                 const unsigned ts = p_now();
                 unsigned n = 0;
                 while (true) {
                     c = __builtin_amdgcn_raw_buffer_load_b64(xr, off, RX_D * 4, kCpNT);
-                    if (__all((c.y >> 11) == want)) break;
+                    if (__all((c.y & kKeyTagMask) == want)) break;
                     if ((++n & 255) == 0) {
                         if (ld_sc1_u(a.ctl + PC_ERR) || p_now() - ts > kSpinTicks) {
                             if ((tid & 63) == 0) atomicMax(a.ctl + PC_ERR, 2u);
@@ -620,10 +620,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                         }
                     }
                 }
-                float bv = __uint_as_float(c.x);
-                int bi = (int)(c.y & 0x7ffu);
-                half_argmax(bv, bi);
+                uint32_t bh = c.x, bl = c.y;
+                half_kmax(bh, bl);  // the 32 slots' candidates: argmax over all classes of row r
                 if (o == 31) {
+                    const int bi = key_cls(bl);
                     float xv;
                     {
 #pragma clang fp contract(off)

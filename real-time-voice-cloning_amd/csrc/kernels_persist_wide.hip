@@ -353,8 +353,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     //    k_p1_expand's fma chain without its zero tap) from the per-frame tables (a.p1q,
     //    runtime.hip pack_p1): the phase's 4 taps, 4 frame rows of Q and one of Aq -- no
     //    [S][B][4H] stream; with WRNN_P1_RING=0 (a.p1q null) copied from that stream instead;
-    //  * the Gumbel noise g = -log q of (tau, row, class u) with k_gumbel's operations
-    //    (philox.h gumbel_of) -- no [S][B][n] noise stream either.
+    //  * the Gumbel noise of (tau, row, class u) in k_gumbel's fixed-point form (philox.h
+    //    gumbel_q_of) -- no [S][B][n] noise stream either.
     auto ring_make = [&](int n, int u, int tau) {
         const int tc = tau < a.S ? tau : a.S - 1;
         int uu = u;
@@ -365,14 +365,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // the noise of class u (a padding class beyond n_classes is drawn and never used)
             const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
             const uint32_t wd = (uu & 3) == 0 ? o.x : (uu & 3) == 1 ? o.y : (uu & 3) == 2 ? o.z : o.w;
-            bst(gumbel_of(wd), rr, (unsigned)WR_G * 4u + cell_i * 4u, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(gumbel_q_of(wd), rr, (unsigned)WR_G * 4u + cell_i * 4u, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);  // (the noise's temporaries die before the P1 loads)
         float4 v;
         if (a.p1q == nullptr) {
+            // (uniform base + 32-bit lane offset: a per-lane 64-bit address spilled)
             v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               mk_rsrc(a.P1 + ((size_t)tc * a.B + g0 + kPG * n) * 4 * kPH),
-                                               (unsigned)uu * 16u, 0, 0));
+                                               mk_rsrc(a.P1 + (size_t)tc * a.B * 4 * kPH),
+                                               ((unsigned)(g0 + kPG * n) * 4u * kPH + (unsigned)uu * 4u) * 4u, 0, 0));
         } else {
             const unsigned p = (unsigned)(ri.rel0 + tc);
             const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
@@ -593,23 +594,24 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         wbar();
         WSTAMP(9);
         if (lo) {
-            const unsigned tag_hi = (seq & kTagSeqMask) << 11;
-            // fc3 epilogue: candidate argmax_k (l_k + g_k) over the slot's 16 classes per row
-            // (row cn = one DPP row of 16 lanes), published tagged by lane cul == 0
+            // fc3 epilogue: the candidate key (persist_common.h cand_key: l_k + G_k in float64)
+            // of the slot's 16 classes per row, max over the row's DPP row of 16 lanes,
+            // published with the step tag by lane cul == 0
             {
-                float val = -INFINITY;
-                int cls = cu;
+                uint32_t kh = 0, kl = 0;
                 if (cell && cu < a.n_classes) {
                     float s;
                     psums(I1(), WL_PS, 1, &s);
                     const float lg = p_add(s, lds[WL_BIAS + 96 + cul]);
                     p_dbg_logit<DBG>(a.dbg, t, crow, cu, a.B, a.n_classes, lg);
-                    val = p_add(lg, pg);
+                    const CandKey k = cand_key(lg, __float_as_uint(pg), cu);
+                    kh = k.hi;
+                    kl = k.lo;
                 }
-                row16_argmax(val, cls);
+                row16_kmax(kh, kl);
                 if (cell && cul == 0)
-                    __builtin_amdgcn_raw_buffer_store_b64((u2v){__float_as_uint(val), tag_hi | (unsigned)cls},
-                                                          xr, wide::cand_off(cn, w), WX_D * 4, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64((u2v){kh, kl | key_tag(seq)}, xr, wide::cand_off(cn, w),
+                                                          WX_D * 4, 0);
             }
             // gh1 = W_hh1 h1 + b_hh1 (for GRU1 below) and gh2 = W_hh2 h2 + b_hh2 (the next GRU2)
             // from the off-path partials, while the candidates travel: every wave wrote them
@@ -634,8 +636,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // row's 16 lanes reduce them (DPP), so every cell of the row holds the sample
             float x;
             {
-                const unsigned want = seq & kTagSeqMask;
-                u4v q = {0u, want << 11, 0u, want << 11};
+                const unsigned want = key_tag(seq);
+                u4v q = {0u, want, 0u, want};
                 const unsigned t0s = p_now();
                 unsigned nsp = 0;
                 while (true) {
@@ -644,7 +646,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                         asm volatile("" : "+v"(vo));
                         q = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, WX_D * 4, kCpNT);
                     }
-                    if (__all((q.y >> 11) == want && (q.w >> 11) == want)) break;
+                    if (__all((q.y & kKeyTagMask) == want && (q.w & kKeyTagMask) == want)) break;
                     if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
                         if (l == 0 && !ld_sc1_u(a.ctl + PC_ERR) &&
                             atomicCAS(a.ctl + PC_WHERE, 0u, wh(9) | ((unsigned)v << 19)) == 0u)
@@ -654,15 +656,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                         break;
                     }
                 }
-                float bv = __uint_as_float(q.x);
-                int bi = (int)(q.y & 0x7ffu);
-                const float v1 = __uint_as_float(q.z);
-                const int k1 = (int)(q.w & 0x7ffu);
-                if (v1 > bv || (v1 == bv && k1 < bi)) {  // ties -> lowest class
-                    bv = v1;
-                    bi = k1;
-                }
-                row16_argmax(bv, bi);
+                uint32_t bh = q.x, bl = q.y;
+                kmax_take(bh, bl, q.z, q.w);
+                row16_kmax(bh, bl);
+                const int bi = key_cls(bl);
                 {
 #pragma clang fp contract(off)
                     x = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;

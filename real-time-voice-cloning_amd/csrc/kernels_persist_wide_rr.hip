@@ -327,8 +327,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                 const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + QL_RI)[n];
                 const int c0 = a.cpw * s + 4 * jq;  // classes c0 .. c0 + 3 (cpw % 4 == 0)
                 const U4 o = philox4x32_10((uint32_t)(c0 >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
-                const u4v gv = {__float_as_uint(gumbel_of(o.x)), __float_as_uint(gumbel_of(o.y)),
-                                __float_as_uint(gumbel_of(o.z)), __float_as_uint(gumbel_of(o.w))};
+                const u4v gv = {gumbel_q_of(o.x), gumbel_q_of(o.y), gumbel_q_of(o.z), gumbel_q_of(o.w)};
                 __builtin_amdgcn_raw_buffer_store_b128(
                     gv, rgr, (unsigned)(RG_P + ((tau & 3) * kRowsW + n) * 64 + 4 * jq) * 4u, 0, 0);
             }
@@ -450,9 +449,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             }
             RS(12);
             // ---- idle while B runs fc5, the sample and GRU1: the partner's ring entry of step
-            // t + 3 (its slot (t + 3) & 3 last held step t - 1, whose reads ended in step t - 1;
-            // the stores drain at this wave's next poll, before any later publication)
+            // t + 3 (its slot (t + 3) & 3 last held step t - 1, whose reads ended in step t - 1).
+            // Waves 4-7 never publish, so B's read-after-x2 ordering needs these stores in L2
+            // before this half's next publication: drained explicitly here (the
+            // wave's next poll would drain them too -- vmcnt counts stores on gfx9 -- but that
+            // is a property of the schedule, not of the code), in an idle window.
             ring_make(t + 3);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             RS(13);
         }
         if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
@@ -605,12 +608,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             qbar();
             RS(11);
             if (v < 4) {
-                const unsigned want = seq & kTagSeqMask;
+                const unsigned want = key_tag(seq);
                 {
-                    // candidate argmax_k (l_k + g_k) over the slot's classes of row cn: lane cul
-                    // takes classes cpw s + 16 j + cul, j < ntc (ascending: ties keep the lowest)
-                    float val = -INFINITY;
-                    int cls = a.cpw * s + cul;
+                    // candidate: the max key (persist_common.h cand_key, l_k + G_k formed exactly)
+                    // over the slot's classes of row cn: lane cul takes classes cpw s + 16 j + cul,
+                    // j < ntc
+                    uint32_t kh = 0, kl = 0;
                     if (cell) {
                         float ps[4];
                         if (ntc == 4)
@@ -624,24 +627,20 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                             if (c < a.n_classes) {
                                 const float lg = p_add(ps[j], cb[96 + 16 * j + cul]);
                                 p_dbg_logit<DBG>(a.dbg, t, crow, c, a.B, a.n_classes, lg);
-                                const float vj = p_add(lg, pn[j]);
-                                if (vj > val) {
-                                    val = vj;
-                                    cls = c;
-                                }
+                                const CandKey k = cand_key(lg, __float_as_uint(pn[j]), c);
+                                kmax_take(kh, kl, k.hi, k.lo);
                             }
                         }
                     }
-                    row16_argmax(val, cls);
+                    row16_kmax(kh, kl);
                     if (cell && cul == 0)
-                        __builtin_amdgcn_raw_buffer_store_b64(
-                            (u2v){__float_as_uint(val), (want << 11) | (unsigned)cls}, xr, q_cand(cn, s), QX_D * 4, 0);
+                        __builtin_amdgcn_raw_buffer_store_b64((u2v){kh, kl | want}, xr, q_cand(cn, s), QX_D * 4, 0);
                 }
                 RS(12);
                 // ---- B7: sample of step t (lanes cul < 8 poll slots 2 cul, 2 cul + 1 of row cn)
                 float x;
                 {
-                    u4v q = {0u, want << 11, 0u, want << 11};
+                    u4v q = {0u, want, 0u, want};
                     const unsigned t0s = p_now();
                     unsigned nsp = 0;
                     const bool pl = cell && cul < 8;
@@ -651,7 +650,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                             asm volatile("" : "+v"(vo));
                             q = __builtin_amdgcn_raw_buffer_load_b128(xr, vo, QX_D * 4, kCpNT);
                         }
-                        if (__all(((q.y >> 11) == want) & ((q.w >> 11) == want))) break;
+                        if (__all(((q.y & kKeyTagMask) == want) & ((q.w & kKeyTagMask) == want))) break;
                         if ((++nsp & 63) == 0 && (ld_sc1_u(a.ctl + PC_ERR) || p_now() - t0s > kSpinTicks)) {
                             if (l == 0 && !ld_sc1_u(a.ctl + PC_ERR) &&
                                 atomicCAS(a.ctl + PC_WHERE, 0u, wh(13) | ((unsigned)v << 19)) == 0u)
@@ -661,10 +660,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                             break;
                         }
                     }
-                    float bv = pl ? __uint_as_float(q.x) : -INFINITY;
-                    int bi = pl ? (int)(q.y & 0x7ffu) : 0x7fffffff;
-                    amax_take(bv, bi, pl ? __uint_as_float(q.z) : -INFINITY, pl ? (int)(q.w & 0x7ffu) : 0x7fffffff);
-                    row16_argmax(bv, bi);
+                    uint32_t bh = pl ? q.x : 0u, bl = pl ? q.y : 0u;
+                    kmax_take(bh, bl, pl ? q.z : 0u, pl ? q.w : 0u);
+                    row16_kmax(bh, bl);
+                    const int bi = key_cls(bl);
                     {
 #pragma clang fp contract(off)
                         x = (2.0f * (float)bi) / (float)(a.n_classes - 1) - 1.0f;
@@ -766,6 +765,17 @@ int wide_rr_layout_check(int R) {
             }
         }
     if (matched != kHalf * R * 4) ++bad;
+    // a cell's own value (x2 = x1 + h2 etc. read the partner half's x of unit 16 s + cul, row cn):
+    // the word o_own = q_prod(s, cn, cul & ~3) + 4 (cul & 3) of the kernel must lie in the packet
+    // published for (slot s, row cn, quad cul & ~3), at the word of unit 16 s + cul
+    for (int s = 0; s < kHalf; ++s)
+        for (int cn = 0; cn < R; ++cn)
+            for (int cul = 0; cul < 16; ++cul) {
+                const unsigned own = q_prod(s, cn, cul & ~3) + 4u * (unsigned)(cul & 3);
+                if (own + 4 > (unsigned)QSLOT * 4u) { ++bad; continue; }
+                const int ow = owner[own / 16];
+                if (ow != (s * kRowsW + cn) * 16 + (cul & ~3) || (int)((own % 16) / 4) != (cul & 3)) ++bad;
+            }
     for (int hb = 0; hb < QN; ++hb)
         for (unsigned sq = 0; sq < 2; ++sq)
             if (q_slot(hb, sq) + (unsigned)QSLOT * 4u > (unsigned)QX_D * 4u ||

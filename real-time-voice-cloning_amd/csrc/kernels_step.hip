@@ -15,6 +15,7 @@
 // the thread that owns the final (unit, row) pair.
 #include "wrnn_kernels.h"
 #include "philox.h"
+#include "cand_key.h"
 
 namespace wrnn {
 
@@ -391,8 +392,7 @@ constexpr int kMaxClassesPerThread = 16;  // n_classes <= 4096 (bits <= 12)
 constexpr int kMaxUnits = 4;              // H <= 1024
 
 __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
-    __shared__ float shf[kWaves];
-    __shared__ int shi[kWaves];
+    __shared__ int shi[2 * kWaves];
     __shared__ float xsh;
     __shared__ uint32_t words[12];
     const int r = blockIdx.x;
@@ -444,66 +444,46 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
     float x = 0.f;
     if (a.t >= 0) {
         if (a.mode == 0) {
-            // 2. Exp(1) noise of this row-step, computed while the logits are in flight
-            float q[kMaxClassesPerThread];
-#pragma unroll
-            for (int i = 0; i < kMaxClassesPerThread; i += 4) {
-                // classes k = tid + (i..i+3)*256 come from 4 different Philox blocks
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int k = tid + (i + u) * kThreads;
-                    q[i + u] = 1.f;
-                    if (k < n) {
-                        const U4 o = philox4x32_10((uint32_t)(k >> 2), (uint32_t)a.t,
-                                                   (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
-                        const uint32_t w = (k & 3) == 0 ? o.x : (k & 3) == 1 ? o.y
-                                         : (k & 3) == 2 ? o.z : o.w;
-                        q[i + u] = exp1_from_u32(w);
-                    }
-                }
-            }
-            // 3. torch softmax + Categorical renormalisation + multinomial fast path:
-            //    k* = argmax((p / sum p) / q)
-            float m = -INFINITY;
-#pragma unroll
-            for (int i = 0; i < kMaxClassesPerThread; ++i) m = fmaxf(m, l[i]);
-            m = block_max(m, shf);
-            float e[kMaxClassesPerThread];
-            float se = 0.f;
+            // 2. the decision (persist_common.h cand_key, the same as the persistent kernels'):
+            //    argmax_k (l_k + G_k), G_k = -log q_k of the contract's Exp(1) variate (philox.h
+            //    gumbel_q_of, computed while the logits are in flight), l + G formed exactly --
+            //    the reference's argmax((softmax(l) / sum) / q) without fp32 rounding of its own
+            uint32_t gq[kMaxClassesPerThread];
 #pragma unroll
             for (int i = 0; i < kMaxClassesPerThread; ++i) {
                 const int k = tid + i * kThreads;
-                e[i] = k < n ? expf(l[i] - m) : 0.f;
-                se += e[i];
+                gq[i] = 0u;
+                if (k < n) {
+                    const U4 o = philox4x32_10((uint32_t)(k >> 2), (uint32_t)a.t, (uint32_t)ri.fold, ri.stream,
+                                               a.k0, a.k1);
+                    const uint32_t w = (k & 3) == 0 ? o.x : (k & 3) == 1 ? o.y : (k & 3) == 2 ? o.z : o.w;
+                    gq[i] = gumbel_q_of(w);
+                }
             }
-            se = block_sum(se, shf);
-            float sp = 0.f;
-#pragma unroll
-            for (int i = 0; i < kMaxClassesPerThread; ++i) {
-                e[i] = e[i] / se;
-                sp += e[i];
-            }
-            sp = block_sum(sp, shf);
-            float best = -INFINITY;
-            int bi = 0x7fffffff;
+            uint32_t bh = 0u, bl = 0u;
 #pragma unroll
             for (int i = 0; i < kMaxClassesPerThread; ++i) {
                 const int k = tid + i * kThreads;
                 if (k < n) {
-                    const float ratio = (e[i] / sp) / q[i];
-                    amax_step(best, bi, ratio, k);
+                    const CandKey c = cand_key(l[i], gq[i], k);
+                    kmax_take(bh, bl, c.hi, c.lo);
                 }
             }
-            wave_argmax_all(best, bi);
+            // wave: DPP rows, then the 4 row results; workgroup: the waves' results via LDS
+            row16_kmax(bh, bl);
+#pragma unroll
+            for (int rr = 16; rr < 64; rr += 16)
+                kmax_take(bh, bl, (uint32_t)__builtin_amdgcn_readlane((int)bh, rr), (uint32_t)__builtin_amdgcn_readlane((int)bl, rr));
             if (lane == 0) {
-                shf[wv] = best;
-                shi[wv] = bi;
+                shi[wv] = (int)bh;
+                shi[kWaves + wv] = (int)bl;
             }
             __syncthreads();
-            float bv = shf[0];
-            int bk = shi[0];
+            bh = (uint32_t)shi[0];
+            bl = (uint32_t)shi[kWaves];
 #pragma unroll
-            for (int w = 1; w < kWaves; ++w) amax_step(bv, bk, shf[w], shi[w]);
+            for (int w = 1; w < kWaves; ++w) kmax_take(bh, bl, (uint32_t)shi[w], (uint32_t)shi[kWaves + w]);
+            const int bk = key_cls(bl);
             {
 #pragma clang fp contract(off)
                 x = (2.0f * (float)bk) / (float)(n - 1) - 1.0f;

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "wrnn_kernels.h"
+#include "cand_key.h"
 
 namespace wrnn {
 
@@ -206,8 +207,8 @@ __device__ __forceinline__ void row16_argmax(float& v, int& k) {
     amax_dpp_step<0x128>(v, k);
 }
 
-// RAW hop D carries its own sequence tag: each slot writes one 64-bit word per row,
-// (value bits, step << 11 | class), so consumers poll the candidates themselves.
+// RAW hop D carries its own sequence tag: each slot writes one 64-bit word per row (the
+// candidate key below, tag in its low byte), so consumers poll the candidates themselves.
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 constexpr unsigned kTagSeqMask = (1u << 21) - 1;  // steps per call < 2^21 (host-checked)
 

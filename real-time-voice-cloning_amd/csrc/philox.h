@@ -44,6 +44,19 @@ __host__ __device__ inline float exp1_from_u32(uint32_t x) {
 __host__ __device__ inline float gumbel_of(uint32_t x) {
     return -logf(exp1_from_u32(x));
 }
+// The sampler's noise since round 5: G = -log q of the same fp32 q (the reference's q tensor is
+// fp32), taken in float64 and stored as a 32-bit fixed-point word, (G + 4) * 2^27 rounded to the
+// nearest integer: q lies in [5.96e-8, 16.64], so G + 4 in [1.19, 20.64] and the word < 2^32;
+// the quantisation error is <= 2^-28 = 3.7e-9 absolute -- below even the last fp32 division of
+// the reference's own p / q (2^-24 relative) -- and the noise still costs 4 bytes per class.
+// persist_common.h cand_key adds it to the fp32 logit in float64.
+constexpr double kGumbelOffset = 4.0;
+constexpr double kGumbelScale = 134217728.0;  // 2^27
+__host__ __device__ inline uint32_t gumbel_q_of(uint32_t x) {
+    const double G = -log((double)exp1_from_u32(x));
+    return (uint32_t)rint((G + kGumbelOffset) * kGumbelScale);
+}
+
 // MOL: torch uniform_(1e-5, 1 - 1e-5) restated on a 24-bit draw (oracle/philox.py mol_uniforms)
 __host__ __device__ inline float mol_uniform_from_u32(uint32_t x) {
     const double U = (double)(x >> 8) * (1.0 / 16777216.0);

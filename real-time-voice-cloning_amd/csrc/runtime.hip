@@ -21,6 +21,7 @@
 #include <tuple>
 #include <vector>
 
+#include "cand_key.h"
 #include "philox.h"
 #include "wavernn_mi355x.h"
 #include "wrnn_kernels.h"
@@ -2914,6 +2915,32 @@ int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row,
     if (!(alpha > 0.f) || !(beta > 0.f)) return fail(WRNN_ERR_INVALID, "alpha, beta must be > 0");
     *out = beta_sample(alpha, beta, step, row, stream, (uint32_t)(seed & 0xffffffffu),
                        (uint32_t)(seed >> 32));
+    return WRNN_OK;
+}
+
+int wrnn_debug_decide(uint64_t seed, uint32_t stream, uint32_t step, uint32_t fold, const float* logits,
+                      int n_classes, int* label, double* margin) {
+    if (!logits || !label) return fail(WRNN_ERR_INVALID, "null argument");
+    if (n_classes < 2 || n_classes > 4096) return fail(WRNN_ERR_INVALID, "n_classes must be in [2, 4096]");
+    const uint32_t k0 = (uint32_t)(seed & 0xffffffffu), k1 = (uint32_t)(seed >> 32);
+    CandKey best{0u, 0u};
+    double v1 = -INFINITY, v2 = -INFINITY;
+    for (int k = 0; k < n_classes; ++k) {
+        const U4 o = philox4x32_10((uint32_t)(k >> 2), step, fold, stream, k0, k1);
+        const uint32_t w = (k & 3) == 0 ? o.x : (k & 3) == 1 ? o.y : (k & 3) == 2 ? o.z : o.w;
+        const uint32_t gq = gumbel_q_of(w);
+        const CandKey c = cand_key(logits[k], gq, k);
+        if (c.hi > best.hi || (c.hi == best.hi && c.lo > best.lo)) best = c;
+        const double v = (double)logits[k] + ((double)gq * (1.0 / kGumbelScale) - kGumbelOffset);
+        if (v > v1) {
+            v2 = v1;
+            v1 = v;
+        } else if (v > v2) {
+            v2 = v;
+        }
+    }
+    *label = key_cls(best.lo);
+    if (margin) *margin = v1 - v2;
     return WRNN_OK;
 }
 

@@ -70,11 +70,18 @@ def _gap(meta, gold, got):
     return min(gaps)
 
 
-def _check(name, meta, gold, got):
+def _check(name, meta, gold, got, labels=None):
+    """`labels`: the call's labels -- a row whose labels left the reference's before a recorded
+    step is no longer teacher-forced there and is left out (trained-like fixtures, where a fold
+    may cross a near-tie: test_gpu_trained.py)."""
     ref = gold['logits']
     assert got.shape == ref.shape, (got.shape, ref.shape)
     assert np.isfinite(got).all(), f'{name}: a recorded logit was never written'
-    err = float(np.abs(got.astype(np.float64) - ref.astype(np.float64)).max())
+    dl = np.abs(got.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)  # (steps, rows)
+    if labels is not None and 'labels' in gold:
+        for i, s in enumerate(gold['logits_steps']):
+            dl[i][(labels[:, :int(s)] != gold['labels'][:, :int(s)]).any(axis=1)] = 0.0
+    err = float(dl.max())
     gap = _gap(meta, gold, got)
     tol = LOGIT_ABS_TOL * max(1.0, float(np.abs(ref).max()))
     print(f'{name}: max |dlogit| {err:.3g} (|logit| <= {np.abs(ref).max():.3g}, tol {tol:.3g}), '
@@ -87,13 +94,13 @@ def _check(name, meta, gold, got):
 @pytest.mark.parametrize('name,engine', CASES)
 def test_logits_match_reference(name, engine):
     meta, gold, m, got = _run(name, engine)
-    _check(name, meta, gold, got)
+    _check(name, meta, gold, got, m.last_labels if meta['mode'] != 'MOL' else None)
 
 
 @pytest.mark.parametrize('name', WIDE)
 def test_wide_logits_match_reference(name, monkeypatch):
     meta, gold, m, got = _run(name, 'persist', wide=True, monkeypatch=monkeypatch)
-    _check(name, meta, gold, got)
+    _check(name, meta, gold, got, m.last_labels)
 
 
 def test_capture_off_and_unrecorded_step():

@@ -22,11 +22,13 @@ def test_dbg_instances_have_production_fp_arithmetic():
     kern = isa_check.kernels_of(isa_check.LIB)
     pairs = isa_check.dbg_pairs(kern)
     names = {p[0].split('I')[0] for p in pairs}
-    # every persistent kernel family has its pairs (k_persist RAW + MOL, rr, gen, wide)
-    for fam in ('_ZN4wrnn9k_persist', '_ZN4wrnn12k_persist_rr', '_ZN4wrnn13k_persist_gen',
-                '_ZN4wrnn14k_persist_wide'):
+    # every persistent kernel family has its pairs (k_persist RAW + MOL, rr, gen, wide, wide_rr)
+    fams = ('_ZN4wrnn9k_persist', '_ZN4wrnn12k_persist_rr', '_ZN4wrnn13k_persist_gen',
+            '_ZN4wrnn14k_persist_wide', '_ZN4wrnn17k_persist_wide_rr')
+    for fam in fams:
         assert any(p[0].startswith(fam + 'I') for p in pairs), fam
-    assert len(pairs) >= 40, names
+    # k_persist 16 RAW + 8 MOL variants, rr 8, gen 12, one each for the two wide kernels
+    assert len(pairs) >= 46, (len(pairs), names)
     for prod, dbg in pairs:
         a, b = isa_check.fp_hist(kern[prod]), isa_check.fp_hist(kern[dbg])
         assert sum(a.values()) > 50, prod
