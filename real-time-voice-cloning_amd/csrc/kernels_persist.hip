@@ -39,6 +39,11 @@
 #ifndef WRNN_PERSIST_PART
 #define WRNN_PERSIST_PART 0
 #endif
+// where the RAW candidate keys are formed: 1 = by the fc3 epilogue lanes, 0 = by wave 0 as it
+// reduces the slot's candidates (A/B)
+#ifndef WRNN_KEY_EPI
+#define WRNN_KEY_EPI 0
+#endif
 
 namespace wrnn {
 
@@ -610,10 +615,25 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             } else {
                 fc3();
             }
-            // [og][r] (logit, noise word) of (row r, class og's); wave 0 forms the candidate keys
-            // (cand_key) as it reduces them -- the float64 sum in this epilogue, beside the fc3
-            // accumulators, spilled the 4-row variant
             float* red = lds + L_RED;
+#if WRNN_KEY_EPI
+            // [og][r] candidate keys (cand_key) of (row r, class og's), formed here by the lanes
+            // that hold the logits; (0, 0) without a class
+            if (kc < NR) {
+                CandKey k{0u, 0u};
+                if (has_cls) {
+                    const float l = p_add(s0, lds[L_BCLS + og]);
+                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    if (MOL)  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
+                        bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
+                    else
+                        k = cand_key(l, __float_as_uint(pgum), cls);
+                }
+                *reinterpret_cast<uint2*>(red + (og * kPNR + kc) * 2) = make_uint2(k.hi, k.lo);
+            }
+#else
+            // [og][r] (logit, noise word) of (row r, class og's); wave 0 forms the candidate keys
+            // (cand_key) as it reduces them
             if (kc < NR) {
                 float l = -INFINITY;
                 if (has_cls) {
@@ -624,6 +644,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 }
                 *reinterpret_cast<float2*>(red + (og * kPNR + kc) * 2) = make_float2(l, pgum);
             }
+#endif
             XSTAMP(28);
             __syncthreads();
             PSTAMP(11);
@@ -638,10 +659,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                         const int r = tt >> 4, o = tt & 15;
                         uint32_t bh = 0, bl = 0;
                         if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+#if WRNN_KEY_EPI
+                            const uint2 k = *reinterpret_cast<const uint2*>(red + (o * kPNR + r) * 2);
+                            bh = k.x;
+                            bl = k.y;
+#else
                             const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
                             const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
                             bh = k.hi;
                             bl = k.lo;
+#endif
                         }
                         row16_kmax(bh, bl);
                         const int rr = r;
@@ -654,10 +681,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                             const int r = rb + (tt >> 5), o = tt & 31;
                             uint32_t bh = 0, bl = 0;
                             if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
+#if WRNN_KEY_EPI
+                                const uint2 k = *reinterpret_cast<const uint2*>(red + (o * kPNR + r) * 2);
+                                bh = k.x;
+                                bl = k.y;
+#else
                                 const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
                                 const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
                                 bh = k.hi;
                                 bl = k.lo;
+#endif
                             }
                             half_kmax(bh, bl);
                             const int rr = r;

@@ -143,8 +143,10 @@ def load_library(path=None):
         'wrnn_debug_wide_layout': (c_int, [c_int]),
         'wrnn_debug_logits': (c_int, [c_void_p, c_int, c_int, P(ctypes.c_float), c_size_t]),
     }
+    # (an A/B build given by WRNN_LIB may predate an entry point: it is left unbound)
+    tolerant = host_only or bool(os.environ.get('WRNN_LIB'))
     for name, (res, args) in sig.items():
-        if host_only and not hasattr(lib, name):
+        if tolerant and not hasattr(lib, name):
             continue
         fn = getattr(lib, name)
         fn.restype = res

@@ -16,6 +16,7 @@ Shapes (BASELINE.json configs[1] and the runtimeracer fork's default topology at
   c2pk  the same with trained-like statistics (tests/golden fatchord_raw9_c2_peaked's knobs)
   rr8   runtimeracer RAW 10-bit, 8 x 1000-frame mels, 6000 / 1000 (232 rows, wide launches);
         utterances 0 and 7 checked
+  rr8pk the same with the trained-like statistics; rr8pk-reg on the register-resident kernel
 Seeds as tools/parity_sweep.py (weights 100 + case, mel 200 + case + 1000 u, noise 300 + case),
 so the round-4 sweep's recorded flips (profiles/r04/parity_sweep/) are among the cases. With
 WRNN_SWEEP_OUT set, one JSON line per utterance is appended there (DESIGN.md §5 numbers).
@@ -35,8 +36,14 @@ SHAPES = {
     'c2pk': dict(topo='fatchord', bits=9, target=11000, overlap=550, utts=1,
                  stats=dict(gru_scale=3.0, fc_scale=2.0, logit_scale=16.0)),
     'rr8': dict(topo='runtimeracer', bits=10, target=6000, overlap=1000, utts=8, stats={}),
+    'rr8pk': dict(topo='runtimeracer', bits=10, target=6000, overlap=1000, utts=8,
+                  stats=dict(gru_scale=3.0, fc_scale=2.0, logit_scale=16.0)),
+    # the same on the register-resident runtimeracer kernel (8 launches of <= 4 rows per group),
+    # its flip count next to the wide kernel's on the same seeds
+    'rr8pk-reg': dict(topo='runtimeracer', bits=10, target=6000, overlap=1000, utts=8,
+                      stats=dict(gru_scale=3.0, fc_scale=2.0, logit_scale=16.0), wide='0'),
 }
-CASES = [(shape, case) for shape in SHAPES for case in range(4)]
+CASES = [(shape, case) for shape in SHAPES for case in range(2 if shape.startswith('rr8pk') else 4)]
 
 
 def _build(shape, case):
@@ -71,7 +78,7 @@ def _run(m, dev, c, nseed, steps=None):
 
 
 @pytest.mark.parametrize('shape,case', CASES, ids=[f'{s}-{c}' for s, c in CASES])
-def test_full_size_sweep_flips_only_at_near_ties(shape, case):
+def test_full_size_sweep_flips_only_at_near_ties(shape, case, monkeypatch):
     import torch
     from oracle.wavernn_oracle import OracleWaveRNN, oracle_infer_waveform
     from near_tie_util import analyse, divergence_steps, first_divergence_per_row
@@ -79,6 +86,8 @@ def test_full_size_sweep_flips_only_at_near_ties(shape, case):
     from wavernn_amd.hparams import sp
     c = SHAPES[shape]
     nseed = 300 + case
+    if 'wide' in c:
+        monkeypatch.setenv('WRNN_PERSIST_WIDE', c['wide'])
     m, hp, sd, mt, mels, dev = _build(shape, case)
     lab_all, roff, _ = _run(m, dev, c, nseed)
     lib = _abi.load_library()
