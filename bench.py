@@ -381,13 +381,22 @@ def main():
                 'fp32_tflops': fl / (us * 1e-6) / 1e12 if us > 0 else None,
                 'fp32_frac': fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS if us > 0 else None,
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
-        if name in ('persist', 'persist_wide'):  # one launch per row batch runs all S steps
-            roof['us_per_step'] = us / S
+        if name in ('persist', 'persist_wide'):
+            # one launch per row batch runs all S steps; a row rotation runs
+            # the call's rows over K launches, S / K steps each on average
+            rot = model.rot_info() if name == 'persist' else (0, 0, 0)
+            steps_launch = S / rot[0] if rot[0] else S
+            roof['us_per_step'] = us / steps_launch
+            if rot[0]:
+                roof['rotation'] = {'launches': rot[0], 'steps_per_launch_hi_rows': rot[1],
+                                    'steps_per_launch_lo_rows': rot[2],
+                                    'us_per_step_note': 'call time / S (the rows rotate through groups of '
+                                                        'q + 1 and q rows, each group at its own step rate)'}
             roof['launches_per_generate'] = sum(r[4] for r in info)
             # MACs per row-step as the runtime counts them (weights of I, rnn*, fc*)
             macs = sum(int(np.prod(v.shape)) for k, v in sd.items()
                        if k.startswith(('I.', 'rnn', 'fc')) and 'weight' in k)
-            rows_l = fl / (S * 2.0 * macs) if S else 0
+            rows_l = fl / (steps_launch * 2.0 * macs) if S else 0
             nr = -(-int(round(rows_l)) // 8)
             floor, hops = latency_floor_us(args.model, hp, nr, model.n_classes,
                                            wide=name == 'persist_wide')

@@ -231,6 +231,18 @@ int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row,
 int wrnn_debug_decide(uint64_t seed, uint32_t stream, uint32_t step, uint32_t fold, const float* logits,
                       int n_classes, int* label, double* margin);
 
+/* Row rotation of the persistent engine: the plan for R fold rows of S steps
+ * given the per-step costs of groups of q + 1 and q rows (q = R / 8), without a device. On
+ * success *launches = K > 0, *n_hi / *n_lo = the steps a group of q + 1 / q rows runs per
+ * launch, and vmap (capacity K * 8 * (q + 1) pairs, may be NULL) receives per launch and
+ * virtual row v = g + 8 r the (physical row, step offset) pair, (-1, -1) for the row slots a
+ * q-row group leaves empty; *launches = 0 when no rotation pays (tests). */
+int wrnn_debug_rot_plan(int rows, int seq_len, double us_hi, double us_lo, int* launches, int* n_hi,
+                        int* n_lo, int* vmap, size_t capacity);
+/* The rotation of the last persistent call: launches (0 = none), steps per launch of the q + 1 /
+ * q-row groups. */
+int wrnn_rot_info(wrnn_handle* h, int* launches, int* n_hi, int* n_lo);
+
 /* Host-side exhaustive check of the wide launch's exchange layout (kernels_persist_wide.hip,
  * csrc/wide_layout.h) for a group of `rows_per_group` rows (1..16): returns the number of
  * violations (0 = every producer packet of a hop lands on exactly the consumer packet that

@@ -75,7 +75,8 @@ constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll ga
 
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
-constexpr int L_BIAS = L_RI + 28;                   // b_hh1, b_hh2 of the slot's units [2][3][16]
+constexpr int L_VM = L_RI + 6 * kPNR;               // (physical row, step offset) of each row slot
+constexpr int L_BIAS = L_VM + 2 * kPNR;             // b_hh1, b_hh2 of the slot's units [2][3][16]
 constexpr int L_W0 = L_BIAS + 96;                    // w0 = W_ih1[:, 0] [512] (GRU1 input term)
 constexpr int L_BCLS = L_W0 + kPH;                  // b_fc3 of the slot's classes [32]
 constexpr int L_W = (L_BCLS + kPCls + 3) & ~3;      // slot weights (kPLdsW4 float4)
@@ -87,23 +88,22 @@ static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 Ki
 
 // P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-template <int NR, bool FC3R, bool MOL, bool P1R, bool DBG>
-__global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_group, s_slot, s_ok;
+// ROT: a rotated launch (PersistArgs::vmap): row slot r of the group is the
+//      virtual row v = g + 8 r, which a.vmap maps to (physical row, step offset of the launch);
+//      the group runs a.giters[g] steps (its rows' steps off .. off + giters - 1). The per-launch
+//      RowInfo table (a.rows, by virtual row) carries rel0 + offset, so every per-frame /
+//      per-position lookup follows; noise, labels, samples, state and logits use the physical
+//      row and the offset step.
+template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG>
+__device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, const int g, const int w) {
+    static_assert(!ROT || P1R, "rotated launches form P1 in the ring");
     const int tid = threadIdx.x;
-    // ---- group formation (placement-independent: a group is whatever shares an XCD) ----
-    if (tid == 0) {
-        int gg, ss;
-        s_ok = p_register(a.ctl, gg, ss);
-        s_group = gg;
-        s_slot = ss;
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const int g = __builtin_amdgcn_readfirstlane(s_group);
-    const int g0 = a.rb + g;  // first fold row of this group in this launch (row batch)
-    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    const int g0 = a.rb + g;  // first (virtual) fold row of this group in this launch
+    // the group's step range: [t0, t1) (rotated: its own step count, offsets per row)
+    const int t1g = ROT ? __builtin_amdgcn_readfirstlane(a.giters[g]) : a.t1;
+    // clamp of the look-ahead loads of noise / conditioning (step indices < tend; past the
+    // group's last step their values go unused)
+    const int tend = ROT ? t1g : a.S;
     const int og = tid >> 4, kc = tid & 15;
     constexpr int H = kPH;
     const int u = 16 * w + (og & 15);   // unit / output of this thread's weight rows
@@ -143,10 +143,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     float h1[NR], h2r = 0.f;
     const bool own = gate_a && kc < NR;
     const int lr = kc < NR ? kc : 0;
-    const int lrow = g0 + kPG * lr;  // row of this lane's epilogue
+    // physical row / step offset of row slot r (identity / 0 unless rotated)
+    auto vmap_g = [&](int r) -> int2 { return ROT ? a.vmap[g0 + kPG * r] : make_int2(g0 + kPG * r, 0); };
+    const int2 lvm = vmap_g(lr);
+    const int lrow = lvm.x;  // (physical) row of this lane's epilogue
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        const int row = g0 + kPG * r;
+        const int row = vmap_g(r).x;
         h1[r] = a.st_h1[(size_t)row * H + tid];
         lds[L_X0 + r * kPH + tid] = a.st_x1[(size_t)row * H + tid];
         lds[L_X1 + r * kPH + tid] = h1[r];
@@ -163,13 +166,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     lds[L_W0 + tid] = a.w0[tid];
     if (tid < 96) lds[L_BIAS + tid] = (tid < 48 ? a.b_hh1 : a.b_hh2)[(tid % 48 / 16) * H + 16 * w + (tid & 15)];
     if ((tid & 15) == 0) lds[L_BCLS + og] = has_cls ? a.b_fc3[cls] : 0.f;
-    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid < NR) {
+        reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+        reinterpret_cast<int2*>(lds + L_VM)[tid] = vmap_g(tid);
+    }
     // per-lane byte offsets (32-bit)
     const unsigned o_tid = (unsigned)tid * 4u;                          // unit tid of a row
     const unsigned o_u = (unsigned)(lr * 5 * kPH + u) * 8u;             // bufA pair (row lr, unit u)
     const unsigned o_y = (unsigned)(lr * kPH + u) * 8u;                 // bufB/C pair (row lr, unit u)
-    // gumbel row lrow (a padding row reads row rb's: no HBM traffic for padding)
-    const unsigned o_gum = (unsigned)((lrow < a.nreal ? lrow : a.rb) * a.n_classes + cls) * 4u;
+    // gumbel row lrow (a padding row reads row rb's: no HBM traffic for padding); a rotated
+    // launch reads its rows' steps off + t: the offset folded into the lane's base
+    const unsigned o_gum = ROT ? (unsigned)(((lvm.y * a.B) + lrow) * a.n_classes + cls) * 4u
+                               : (unsigned)((lrow < a.nreal ? lrow : a.rb) * a.n_classes + cls) * 4u;
     const rsrc_t fcr = mk_rsrc(a.fcond);
     __syncthreads();
 
@@ -210,7 +218,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         asm volatile("" : "+v"(tx));
         const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15);
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kx >> 2];
-        tau = tau < a.S ? tau : a.S - 1;
+        // (a row's own steps end at S: a rotated row at offset off reads P1 up to S - 1 - off;
+        // the P1 of the step after the launch's last one feeds the GRU1 whose state is saved)
+        const int lim = ROT ? a.S - reinterpret_cast<const int2*>(lds + L_VM)[kx >> 2].y : a.S;
+        tau = tau < lim ? tau : lim - 1;
         const unsigned p = (unsigned)(ri.rel0 + tau);
         const bool in = p < (unsigned)ri.L;  // else the zero tail pad: bias only (zero frame)
         const unsigned f = p / (unsigned)a.hop, sph = in ? p - f * (unsigned)a.hop : 0u;
@@ -258,7 +269,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 pC[r] = __uint_as_float(v.w);
             }
         }
-        te = te < a.S ? te : a.S - 1;
+        te = te < tend ? te : tend - 1;
         if (kc < NR) {
             int uu = u;  // (offsets recomputed per step: hoisted ones cost registers)
             asm volatile("" : "+v"(uu));
@@ -278,10 +289,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         // MOL: sampling lane (row r, k < 11) holds draw k of its row (k_mol_noise)
         if (MOL) {
             const int sl = EARLY ? tid - 256 : tid;
-            const int mrow = g0 + kPG * (sl >> 5);
-            if (sl >= 0 && sl < 32 * NR && (sl & 31) < 11)
-                pgn = bld(mk_rsrc(a.gumbel + ((size_t)te * a.B + (mrow < a.nreal ? mrow : a.rb)) * kMolNoise),
+            if (sl >= 0 && sl < 32 * NR && (sl & 31) < 11) {
+                const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[sl >> 5];
+                const int mrow = ROT ? vm.x : (vm.x < a.nreal ? vm.x : a.rb);
+                pgn = bld(mk_rsrc(a.gumbel + ((size_t)(te + vm.y) * a.B + mrow) * kMolNoise),
                           (unsigned)(sl & 31) * 4u, 0);
+            }
         }
     };
     if (tid == 0) lds[L_FAIL] = 0.f;
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     __syncthreads();
     const int tl = tid & 255;  // index inside the half that stages
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
-    for (int t = a.t0; t < a.t1; ++t) {
+    for (int t = a.t0; t < t1g; ++t) {
         const unsigned seq = (unsigned)t + 1u;
         const unsigned sA = (unsigned)(XB_A + (t & 1) * XB_A_SZ) * 4u;  // bufA of this step
         PSTAMP(0);
@@ -623,7 +636,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 CandKey k{0u, 0u};
                 if (has_cls) {
                     const float l = p_add(s0, lds[L_BCLS + og]);
-                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t + lvm.y, lrow, cls, a.B, a.n_classes, l);
                     if (MOL)  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
                         bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
                     else
@@ -638,7 +651,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 float l = -INFINITY;
                 if (has_cls) {
                     l = p_add(s0, lds[L_BCLS + og]);
-                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t + lvm.y, lrow, cls, a.B, a.n_classes, l);
                     if (MOL)  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
                         bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
                 }
@@ -751,7 +764,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                     if (w == 0) {
                         int rr = r;  // (recomputed per step: a hoisted offset costs a register)
                         asm volatile("" : "+v"(rr));
-                        const unsigned ro = (unsigned)((g0 + kPG * rr) * a.ld);
+                        const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[rr];
+                        const unsigned ro = (unsigned)(vm.x * a.ld + vm.y);
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
                                                               ro * 2u, (unsigned)t * 2u, 0);
                         bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -809,8 +823,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
                 if (w == 0) {
                     int rr = r;
                     asm volatile("" : "+v"(rr));
-                    const int row = g0 + kPG * rr;
-                    bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+                    const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[rr];
+                    bst(xv, mk_rsrc(a.samples), (unsigned)(vm.x * a.ld + vm.y) * 4u, (unsigned)t * 4u);
                 }
             }
         }
@@ -837,7 +851,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
         }
         pgum = pgn;
         if (w == 0 && tid == 0) {
-            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            // (rotated: the launch's share of the call, steps scaled to S per launch)
+            if (g == 0) p_progress(a.progress, a.prog_base, ROT ? (int)((long long)t * a.S / t1g) : t, t);
             if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen after the next sample
         }
         __syncthreads();
@@ -848,14 +863,14 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
     // ---- save the chunk state --------------------------------------------------------------
     // (addresses recomputed here: values kept alive across the step loop cost registers)
-    if (a.t1 < a.S) {
+    if (ROT || a.t1 < a.S) {
         int tx = tid;
         asm volatile("" : "+v"(tx));
-        const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15), rx = g0 + kPG * (kx < NR ? kx : 0);
+        const int kx = tx & 15, ux = 16 * w + ((tx >> 4) & 15), rx = vmap_g(kx < NR ? kx : 0).x;
         if (w == 0)
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                const int row = g0 + kPG * r;
+                const int row = vmap_g(r).x;
                 a.st_x1[(size_t)row * H + tx] = lds[L_X0 + r * kPH + tx];
                 a.st_h1[(size_t)row * H + tx] = lds[L_X1 + r * kPH + tx];
             }
@@ -865,6 +880,32 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
             for (int j = 0; j < 3; ++j)
                 a.st_gh2[(size_t)rx * 3 * H + j * H + ux] = lds[L_GH2 + (og * 3 + j) * kPNR + kc];
         }
+    }
+}
+
+template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG>
+__global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    // ---- group formation (placement-independent: a group is whatever shares an XCD) ----
+    if (threadIdx.x == 0) {
+        int gg, ss;
+        s_ok = p_register(a.ctl, gg, ss);
+        s_group = gg;
+        s_slot = ss;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    if constexpr (ROT && NR > 1) {
+        // a rotated launch holds groups of NR and of NR - 1 rows: each runs its own body
+        if (__builtin_amdgcn_readfirstlane(a.gnr[g]) == NR)
+            persist_body<NR, FC3R, MOL, P1R, true, DBG>(a, lds, g, w);
+        else
+            persist_body<NR - 1, FC3R, MOL, P1R, true, DBG>(a, lds, g, w);
+    } else {
+        persist_body<NR, FC3R, MOL, P1R, ROT, DBG>(a, lds, g, w);
     }
 }
 
@@ -961,16 +1002,58 @@ size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
-    if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, true>>(persist_lds_bytes(), a, s);
-    return persist_launch<k_persist<NR, FC3R, MOL, P1R, false>>(persist_lds_bytes(), a, s);
+    if constexpr (P1R && !FC3R && NR >= 2) {  // rotated launches (a.vmap): 9-bit ring variants
+        if (a.vmap) {
+            if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, true, true>>(persist_lds_bytes(), a, s);
+            return persist_launch<k_persist<NR, FC3R, MOL, P1R, true, false>>(persist_lds_bytes(), a, s);
+        }
+    }
+    if (a.vmap) return hipErrorInvalidValue;
+    if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, false, true>>(persist_lds_bytes(), a, s);
+    return persist_launch<k_persist<NR, FC3R, MOL, P1R, false, false>>(persist_lds_bytes(), a, s);
 }
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 int persist_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R, false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R, false, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
+
+// scratch bytes of the rotated instance (groups of NR and NR - 1 rows); -1 when none exists
+template <int NR, bool MOL>
+int persist_rot_spill_t() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, false, MOL, true, true, false>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+#if WRNN_PERSIST_PART != 1
+int persist_rot_scratch_mol(int nr) {
+    switch (nr) {
+        case 2: return persist_rot_spill_t<2, true>();
+        case 3: return persist_rot_spill_t<3, true>();
+        case 4: return persist_rot_spill_t<4, true>();
+        default: return -1;
+    }
+}
+#else
+int persist_rot_scratch_mol(int nr);
+#endif
+
+#if WRNN_PERSIST_PART != 2
+// Scratch bytes of the rotated instance with groups of nr and nr - 1 rows (9-bit RAW or MOL,
+// P1 ring); -1 when none exists.
+int persist_rot_scratch(int nr, int mode) {
+    if (mode != 0) return persist_rot_scratch_mol(nr);
+    switch (nr) {
+        case 2: return persist_rot_spill_t<2, false>();
+        case 3: return persist_rot_spill_t<3, false>();
+        case 4: return persist_rot_spill_t<4, false>();
+        default: return -1;
+    }
+}
+#endif
 
 #if WRNN_PERSIST_PART != 1
 // MOL variants (30 classes: cpw <= 16)

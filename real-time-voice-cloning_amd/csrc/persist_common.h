@@ -145,10 +145,11 @@ inline hipError_t persist_launch(size_t lds, const Args& a, hipStream_t s) {
 // back at i % 100 == 0): after step t with t % 100 == 0, one lane publishes base + t + 1
 // steps done to a host-mapped word (vector store, system scope); the host polls it while the
 // launch runs. base = row batch * S.
-__device__ __forceinline__ void p_progress(unsigned* prog, int base, int t) {
+__device__ __forceinline__ void p_progress(unsigned* prog, int base, int value, int t) {
     if (prog != nullptr && t % kProgressEvery == 0)
-        __hip_atomic_store(prog, (unsigned)(base + t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(prog, (unsigned)(base + value + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void p_progress(unsigned* prog, int base, int t) { p_progress(prog, base, t, t); }
 
 // Abort request of the host (the progress callback returned non-zero): the host sets the
 // host-mapped word kAbortWord words past the progress word. At its progress points (every 100

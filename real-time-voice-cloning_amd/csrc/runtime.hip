@@ -209,7 +209,7 @@ struct wrnn_handle {
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
     } pw;
     struct PersistWS {
-        DevBuf P1, gumbel, ctl, xbuf, st, stamps, phases, wring;
+        DevBuf P1, gumbel, ctl, xbuf, st, stamps, phases, wring, rot;
     } pws;
     int engine = WRNN_ENGINE_AUTO;  // requested engine (wrnn_set_engine / env WRNN_ENGINE)
     int last_engine = WRNN_ENGINE_CHAIN;
@@ -223,12 +223,21 @@ struct wrnn_handle {
     struct PLaunch {
         int rb, nr;  // first row, rows per XCD group (the launch runs rows rb + g + 8 r, r < nr)
         bool wide;   // kernels_persist_wide.hip (MFMA) or the register-resident kernel
+        int rot = -1;  // launch j of the call's row rotation (rot_plan), or -1
     };
+    // Row rotation of the last call: per launch j the virtual-row map
+    // (physical row, step offset), rows and steps per group, and the launch's RowInfo table
+    struct RotPlan {
+        int K = 0, nr_hi = 0, n_hi = 0, n_lo = 0;
+        std::vector<int2> vmap;     // [K][kPG * nr_hi]
+        std::vector<int> gnr, git;  // [K][kPG]
+    } rot_plan;
     std::vector<PLaunch> p_plan;    // PERSIST: the launches of the last call, in order
     std::vector<int> pev_kind;      // per timed launch: 1 wide, 0 otherwise
     std::vector<int> pev_rows;      // per timed launch: rows (8 nr)
     std::vector<hipEvent_t> pev;    // PERSIST timing events (start, end) per launch
-    std::vector<int> pev_steps;
+    std::vector<double> pev_steps;
+    std::vector<char> rot_host;     // the row rotation's per-launch tables (uploaded per call)
     double p_step_bytes = 0, p_step_flops = 0;  // algorithmic per step
     double p_wbytes = 0, p_row_bytes = 0, p_macs = 0;  // per step: weights, per row-step, MACs/row
     struct PStage {
@@ -1802,6 +1811,71 @@ void persist_wide_rr_phase_report(wrnn_handle* h, int t) {
     }
 }
 
+// Row rotation. R fold rows on the 8 XCD groups of one register-resident
+// launch leave m = R % 8 groups with q + 1 rows and 8 - m with q: every group pays the
+// (q + 1)-row step (a padding row costs as much as a real one), so the launch runs S steps at
+// t(q + 1). Rotating the rows through the q + 1-row groups over K launches -- each row spends
+// h_c of them in a q + 1-row group and l_c in a q-row group, a group of q rows running its own
+// q-row body (the rotated kernel instance holds both) -- lets every group run at its own rate:
+// a q + 1-row group runs n_hi steps, a q-row group n_lo, n_hi t(q + 1) ~ n_lo t(q), and
+// h_c n_hi + l_c n_lo = S for every row. A row's state crosses launches through the chunk state
+// (st_*); its noise, labels and frames are read at its own step (the map's offset).
+// C2 (18 rows): 3 launches, 3672 steps at 3 rows / 4214 at 2 -> 65.1 ms instead of 71.5.
+static int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
+
+bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan& P) {
+    P = wrnn_handle::RotPlan();
+    const int q = R / kPG, m = R % kPG;
+    if (q < 1 || m == 0 || q + 1 > 3 || S < 64) return false;
+    const int H = m * (q + 1), gg = gcd_i(R, H), K = R / gg, hc = H / gg, lc = K - hc;
+    if (K > 24 || lc < 1) return false;
+    // n_hi t_hi = n_lo t_lo and hc n_hi + lc n_lo = S, in integers
+    const double nh0 = S / (hc + lc * t_hi / t_lo);
+    int nh = -1, nl = -1;
+    for (int d = 0; d <= lc && nh < 0; ++d)
+        for (int sgn = -1; sgn <= 1 && nh < 0; sgn += 2) {
+            const int c = (int)std::lround(nh0) + sgn * d;
+            if (c >= 1 && (S - hc * c) > 0 && (S - hc * c) % lc == 0) {
+                nh = c;
+                nl = (S - hc * c) / lc;
+            }
+        }
+    if (nh < 1 || nl < 1) return false;
+    // worth it? (an extra launch reloads the weights: ~40 us)
+    const double rot = K * std::max(nh * t_hi, nl * t_lo) + (K - 1) * 40.0, plain = S * t_hi;
+    if (rot > 0.98 * plain) return false;
+    P.K = K;
+    P.nr_hi = q + 1;
+    P.n_hi = nh;
+    P.n_lo = nl;
+    P.vmap.assign((size_t)K * kPG * (q + 1), make_int2(0, 0));
+    P.gnr.assign((size_t)K * kPG, 0);
+    P.git.assign((size_t)K * kPG, 0);
+    std::vector<int> off(R, 0);
+    for (int j = 0; j < K; ++j) {
+        std::vector<char> hi(R, 0);
+        std::vector<int> his, los;
+        for (int i = 0; i < H; ++i) hi[(j * gg + i) % R] = 1;
+        for (int i = 0; i < H; ++i) his.push_back((j * gg + i) % R);
+        for (int r = 0; r < R; ++r)
+            if (!hi[r]) los.push_back(r);
+        for (int g = 0; g < kPG; ++g) {
+            const bool gh = g < m;
+            const int nr = gh ? q + 1 : q;
+            P.gnr[(size_t)j * kPG + g] = nr;
+            P.git[(size_t)j * kPG + g] = gh ? nh : nl;
+            for (int r = 0; r < nr; ++r) {
+                const int row = gh ? his[(size_t)g * (q + 1) + r] : los[(size_t)(g - m) * q + r];
+                P.vmap[(size_t)j * kPG * (q + 1) + g + kPG * r] = make_int2(row, off[row]);
+            }
+        }
+        for (int r = 0; r < R; ++r) off[r] += hi[r] ? nh : nl;
+    }
+    for (int r = 0; r < R; ++r)
+        if (off[r] != S) return (P = wrnn_handle::RotPlan(), false);
+    return true;
+}
+
 // PERSIST engine: P1 for all steps (one MFMA GEMM), Gumbel noise (RAW), step-0 state, then
 // the persistent recurrence in chunks (one chunk per call unless a progress callback wants
 // reports; every 1000 steps then).
@@ -1821,6 +1895,7 @@ int persist_noise(wrnn_handle* h, int S, hipStream_t st) {
         any_wide |= L.wide;
         any_reg |= !L.wide;
     }
+    // (a rotated plan has only register-resident launches over the same rows: any_wide false)
     if (raw && any_wide && !any_reg) {  // every launch draws its noise in-kernel
         CHECK(P.gumbel.alloc(sizeof(float)));
         return WRNN_OK;
@@ -2031,6 +2106,32 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     h->pev_kind.clear();
     h->pev_rows.clear();
     if (h->timing) CHECK(P.stamps.alloc((size_t)nb * 2 * sizeof(uint32_t)));
+    // row rotation: per launch j the virtual-row map, rows / steps per group and the RowInfo
+    // table by virtual row (rel0 advanced by the row's offset), one device block per launch
+    const auto& RP = h->rot_plan;
+    const bool rotp = nb > 0 && h->p_plan[0].rot >= 0;
+    size_t rot_stride = 0;
+    if (rotp) {
+        const int nv = kPG * RP.nr_hi;
+        const size_t o_gnr = (size_t)nv * sizeof(int2), o_git = o_gnr + kPG * sizeof(int),
+                     o_rows = o_git + kPG * sizeof(int);
+        rot_stride = (o_rows + (size_t)nv * sizeof(RowInfo) + 255) & ~(size_t)255;
+        h->rot_host.assign(rot_stride * RP.K, 0);
+        for (int j = 0; j < RP.K; ++j) {
+            char* base = h->rot_host.data() + rot_stride * j;
+            std::memcpy(base, &RP.vmap[(size_t)j * nv], (size_t)nv * sizeof(int2));
+            std::memcpy(base + o_gnr, &RP.gnr[(size_t)j * kPG], kPG * sizeof(int));
+            std::memcpy(base + o_git, &RP.git[(size_t)j * kPG], kPG * sizeof(int));
+            RowInfo* rv = reinterpret_cast<RowInfo*>(base + o_rows);
+            for (int v = 0; v < nv; ++v) {
+                const int2 m = RP.vmap[(size_t)j * nv + v];
+                rv[v] = h->rows_host[m.x];
+                rv[v].rel0 += m.y;
+            }
+        }
+        CHECK(P.rot.alloc(h->rot_host.size()));
+        HIPC(hipMemcpyAsync(P.rot.p, h->rot_host.data(), h->rot_host.size(), hipMemcpyHostToDevice, st));
+    }
     const auto t_start = std::chrono::steady_clock::now();
     for (int b = 0; b < nb; ++b) {
         const auto& L = h->p_plan[b];
@@ -2039,6 +2140,18 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.t0 = 0;
         a.t1 = S;
         a.prog_base = b * S;
+        a.vmap = nullptr;
+        a.gnr = a.giters = nullptr;
+        a.rows = (const RowInfo*)ws.rows.p;
+        if (L.rot >= 0) {
+            const char* base = (const char*)P.rot.p + rot_stride * L.rot;
+            const int nv = kPG * RP.nr_hi;
+            a.vmap = (const int2*)base;
+            a.gnr = (const int*)(base + (size_t)nv * sizeof(int2));
+            a.giters = a.gnr + kPG;
+            a.rows = (const RowInfo*)(base + (size_t)nv * sizeof(int2) + 2 * kPG * sizeof(int));
+            a.t1 = std::max(RP.n_hi, RP.n_lo);
+        }
         if (L.wide)  // sentinel-initialised vector slots (kernels_persist_wide*.hip polls)
             HIPC(rr ? persist_wide_rr_reset_xbuf(P.xbuf.f(), st) : persist_wide_reset_xbuf(P.xbuf.f(), st));
         else
@@ -2053,7 +2166,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             HIPC(hipEventCreate(&e1));
             h->pev.push_back(e0);
             h->pev.push_back(e1);
-            h->pev_steps.push_back(S);
+            h->pev_steps.push_back(L.rot >= 0 ? (double)S / RP.K : (double)S);  // (rotation: S per call)
             h->pev_kind.push_back(L.wide ? 1 : 0);
             h->pev_rows.push_back(kPG * L.nr);
             HIPC(hipEventRecord(e0, st));
@@ -2320,7 +2433,9 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         };
         std::vector<Opt> opts;
         if (!h->pw.gen && !h->pw.rr) {
-            static const double us[2][kPNR + 1] = {{0, 4.8, 5.6, 6.7, 8.3}, {0, 4.9, 5.64, 7.7, 9.4}};
+            // measured MI355X us per step by rows per group (9-bit: round 5, tools/nr_probe.sh;
+            // 10-bit: round 2)
+            static const double us[2][kPNR + 1] = {{0, 4.8, 5.15, 5.91, 6.92}, {0, 4.9, 5.64, 7.7, 9.4}};
             const int w10 = h->pw.cpw > 16 ? 1 : 0;
             for (int c = 1; c <= kPNR; ++c) {
                 int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 0);
@@ -2421,6 +2536,23 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
                 persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
             h->p1_ring = false;
+    // row rotation (plan_rotation): one register-resident 9-bit launch with
+    // uneven groups becomes K launches over rotating row sets (WRNN_PERSIST_ROT=0: off)
+    h->rot_plan = wrnn_handle::RotPlan();
+    if (use_p && h->p1_ring && h->p_plan.size() == 1 && !h->p_plan[0].wide && !h->pw.rr && !h->pw.gen &&
+        h->pw.cpw <= 16 && (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL)) {
+        const char* env = std::getenv("WRNN_PERSIST_ROT");
+        const int nr = h->p_plan[0].nr;
+        static const double us9[kPNR + 1] = {0, 4.8, 5.15, 5.91, 6.92};
+        // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
+        // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
+        const int rs = nr >= 2 ? persist_rot_scratch(nr, h->cfg.mode) : -1;
+        if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
+            plan_rotation(B, S, us9[nr], us9[nr - 1], h->rot_plan)) {
+            h->p_plan.clear();
+            for (int j = 0; j < h->rot_plan.K; ++j) h->p_plan.push_back({0, nr, false, j});
+        }
+    }
     h->p1_stream = use_p && !h->p1_ring;  // (the wide launches form P1 in-kernel too)
     if (h->p1_stream && h->pw.rr && rr_frames_ok(h)) {  // runtimeracer: only wide launches
         bool all_wide = !h->p_plan.empty();                // form P1 in-kernel
@@ -2915,6 +3047,41 @@ int wrnn_debug_beta(uint64_t seed, uint32_t stream, uint32_t step, uint32_t row,
     if (!(alpha > 0.f) || !(beta > 0.f)) return fail(WRNN_ERR_INVALID, "alpha, beta must be > 0");
     *out = beta_sample(alpha, beta, step, row, stream, (uint32_t)(seed & 0xffffffffu),
                        (uint32_t)(seed >> 32));
+    return WRNN_OK;
+}
+
+int wrnn_debug_rot_plan(int rows, int seq_len, double us_hi, double us_lo, int* launches, int* n_hi,
+                        int* n_lo, int* vmap, size_t capacity) {
+    if (!launches || !n_hi || !n_lo) return fail(WRNN_ERR_INVALID, "null argument");
+    if (rows < 1 || seq_len < 1 || !(us_hi > 0) || !(us_lo > 0)) return fail(WRNN_ERR_INVALID, "bad arguments");
+    wrnn_handle::RotPlan P;
+    *launches = *n_hi = *n_lo = 0;
+    if (!plan_rotation(rows, seq_len, us_hi, us_lo, P)) return WRNN_OK;
+    const int q = rows / kPG, nv = kPG * P.nr_hi;
+    if (vmap) {
+        if (capacity < (size_t)P.K * nv * 2) return fail(WRNN_ERR_CAPACITY, "capacity");
+        for (int j = 0; j < P.K; ++j)
+            for (int v = 0; v < nv; ++v) {
+                const int g = v % kPG, r = v / kPG;
+                const bool used = r < P.gnr[(size_t)j * kPG + g];
+                const int2 m = P.vmap[(size_t)j * nv + v];
+                vmap[((size_t)j * nv + v) * 2] = used ? m.x : -1;
+                vmap[((size_t)j * nv + v) * 2 + 1] = used ? m.y : -1;
+            }
+    }
+    (void)q;
+    *launches = P.K;
+    *n_hi = P.n_hi;
+    *n_lo = P.n_lo;
+    return WRNN_OK;
+}
+
+int wrnn_rot_info(wrnn_handle* h, int* launches, int* n_hi, int* n_lo) {
+    if (!h || !launches || !n_hi || !n_lo) return fail(WRNN_ERR_INVALID, "null argument");
+    const bool rot = !h->p_plan.empty() && h->p_plan[0].rot >= 0 && h->last_engine == WRNN_ENGINE_PERSIST;
+    *launches = rot ? h->rot_plan.K : 0;
+    *n_hi = rot ? h->rot_plan.n_hi : 0;
+    *n_lo = rot ? h->rot_plan.n_lo : 0;
     return WRNN_OK;
 }
 

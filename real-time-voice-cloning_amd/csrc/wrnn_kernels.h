@@ -241,6 +241,12 @@ struct PersistArgs {
     const float4* wwide_lds;// [kPM][2 tiles][8][4][64] (W_hh2 z, n)
     float* wring;           // wide launches: per-group ring of P1 and noise (persist_wide_ring_floats)
     DbgLogits dbg;
+    // rotated launch (k_persist; null otherwise): virtual row v = g + 8 r ->
+    // (physical row, step offset), rows per group (nr or nr - 1), steps per group; `rows` is then
+    // the launch's RowInfo table by virtual row (rel0 advanced by the offset)
+    const int2* vmap;
+    const int* gnr;
+    const int* giters;
 };
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
@@ -381,6 +387,7 @@ hipError_t launch_gumbel_rows(float* g, int S, int r0, int nrows, int ld, int n_
 // ring: the P1-ring variant (PersistArgs::p1q set) or the P1-stream variant
 int persist_variant_ok(int nr, int cpw, int mode, int ring);
 int persist_variant_scratch(int nr, int cpw, int mode, int ring);
+int persist_rot_scratch(int nr, int mode);  // rotated instance (groups of nr and nr - 1 rows)
 size_t persist_lds_bytes();
 size_t persist_xbuf_floats();
 

@@ -214,6 +214,13 @@ class WaveRNN:
         _abi.check(self._lib.wrnn_plan_info(self._h, ctypes.byref(n), fr, nr, wd, cap))
         return [(fr[i], nr[i], bool(wd[i])) for i in range(min(n.value, cap))]
 
+    def rot_info(self):
+        """Row rotation of the last persistent call: (launches, steps per
+        launch of the q + 1-row groups, of the q-row groups); (0, 0, 0) when none."""
+        k, nh, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _abi.check(self._lib.wrnn_rot_info(self._h, ctypes.byref(k), ctypes.byref(nh), ctypes.byref(nl)))
+        return k.value, nh.value, nl.value
+
     def fallback_info(self):
         """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
         n = ctypes.c_int()

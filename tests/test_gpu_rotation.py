@@ -1,0 +1,106 @@
+"""Row rotation of the persistent engine on the GPU: a call whose rows leave the
+XCD groups uneven (R % 8 != 0) runs as K launches over rotating row sets, groups of q rows on
+their own q-row body. The rotation only moves WHERE and WHEN a row's steps run: every row's
+arithmetic is the same, so the labels / samples must equal the single-launch plan's
+(WRNN_PERSIST_ROT=0) bit for bit -- RAW and MOL, several row counts, with logit capture (the
+DBG instances) and with the reference's progress callback. Full-size parity against the oracle
+with the rotation on is tests/test_gpu_fullsize.py (C2 is rotated by default).
+Reference: vocoder/models/fatchord_version.py:192-236 (the step), :234-236 (progress)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TARGET, OVERLAP = 4000, 400  # 4,800 steps (shorter calls do not pay for the extra launches)
+
+
+def _model(mode='RAW'):
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.model import WaveRNN
+    from wavernn_amd.synth import synth_state_dict
+    hp = hparams_for('fatchord-wavernn').copy(bits=9, mode=mode)
+    m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels, hp.compute_dims,
+                hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate, mode=mode,
+                model_type='fatchord-wavernn', device=0)
+    m.load_state_dict(synth_state_dict(hp, 'fatchord-wavernn', seed=11))
+    m.set_engine('persist')
+    return m, hp
+
+
+def _frames_for(m, rows):
+    for T in range(2, 2000):
+        if m.fold_shape(T, True, TARGET, OVERLAP)[0] == rows:
+            return T
+    raise AssertionError(rows)
+
+
+def _call(m, mel, monkeypatch, rot, debug_steps=None, cb=None):
+    import torch
+    from wavernn_amd.hparams import sp
+    monkeypatch.setenv('WRNN_PERSIST_ROT', '1' if rot else '0')
+    m.set_seed(77)
+    m.set_debug_steps(debug_steps)
+    try:
+        if cb is None:
+            dev = torch.from_numpy((mel / sp.max_abs_value).astype(np.float32)).cuda()
+            out, roff, S = m.generate_batch_device([dev], True, TARGET, OVERLAP)
+            res = out.cpu().numpy()
+        else:
+            m.generate((mel / sp.max_abs_value)[None], True, TARGET, OVERLAP, True, True, progress_callback=cb)
+            res = m.last_labels if m.last_labels is not None else m.last_samples
+        logs = {s: m.debug_logits(s, range(res.shape[0])) for s in (debug_steps or [])}
+        return res, m.rot_info(), logs
+    finally:
+        m.set_debug_steps(None)
+
+
+@pytest.mark.parametrize('rows', [9, 10, 17, 18, 20])
+def test_rotated_labels_equal_single_launch(rows, monkeypatch):
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    mel = synth_mel(_frames_for(m, rows), 500 + rows)
+    a, ra, _ = _call(m, mel, monkeypatch, rot=True)
+    b, rb, _ = _call(m, mel, monkeypatch, rot=False)
+    assert a.shape[0] == rows and ra[0] > 1 and rb[0] == 0, (a.shape, ra, rb)
+    d = np.argwhere(a != b)
+    assert len(d) == 0, f'{rows} rows: first difference {d[np.argmin(d[:, 1])].tolist()}'
+
+
+def test_rotated_mol_samples_equal_single_launch(monkeypatch):
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model('MOL')
+    mel = synth_mel(_frames_for(m, 18), 77)
+    a, ra, _ = _call(m, mel, monkeypatch, rot=True)
+    b, rb, _ = _call(m, mel, monkeypatch, rot=False)
+    assert ra[0] > 1 and rb[0] == 0
+    assert np.array_equal(a, b)
+
+
+def test_rotated_logit_capture_equals_single_launch(monkeypatch):
+    """The DBG instances record each row's logits at its own step (the offset step)."""
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    mel = synth_mel(_frames_for(m, 18), 3)
+    # around the launch boundaries (18 rows, 4,800 steps: 1,456 steps at 3 rows, 1,672 at 2)
+    steps = [0, 1455, 1456, 1672, 3128, 3129, 3344, 4799]
+    a, ra, la = _call(m, mel, monkeypatch, rot=True, debug_steps=steps)
+    b, rb, lb = _call(m, mel, monkeypatch, rot=False, debug_steps=steps)
+    assert ra[0] > 1 and np.array_equal(a, b)
+    for s in steps:
+        assert np.isfinite(la[s]).all(), s
+        assert np.array_equal(la[s], lb[s]), s
+
+
+def test_rotated_call_reports_progress_at_the_reference_cadence(monkeypatch):
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    mel = synth_mel(_frames_for(m, 18), 5)
+    seen = []
+    a, ra, _ = _call(m, mel, monkeypatch, rot=True, cb=lambda i, n, b, r: seen.append((i, n, b)))
+    S = a.shape[1]
+    assert ra[0] > 1
+    assert [s[0] for s in seen] == list(range(0, S, 100))
+    assert all(n == S and b == 18 for _, n, b in seen)
+    b_, rb, _ = _call(m, mel, monkeypatch, rot=False)
+    assert np.array_equal(a, b_)

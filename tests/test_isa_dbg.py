@@ -27,8 +27,9 @@ def test_dbg_instances_have_production_fp_arithmetic():
             '_ZN4wrnn14k_persist_wide', '_ZN4wrnn17k_persist_wide_rr')
     for fam in fams:
         assert any(p[0].startswith(fam + 'I') for p in pairs), fam
-    # k_persist 16 RAW + 8 MOL variants, rr 8, gen 12, one each for the two wide kernels
-    assert len(pairs) >= 46, (len(pairs), names)
+    # k_persist 16 RAW + 8 MOL variants + 6 rotated (NR 2-4, RAW / MOL), rr 8, gen 12, one
+    # each for the two wide kernels
+    assert len(pairs) >= 52, (len(pairs), names)
     for prod, dbg in pairs:
         a, b = isa_check.fp_hist(kern[prod]), isa_check.fp_hist(kern[dbg])
         assert sum(a.values()) > 50, prod
