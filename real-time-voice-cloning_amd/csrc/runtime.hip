@@ -2544,11 +2544,14 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
         static const double us9[kPNR + 1] = {0, 4.8, 5.15, 5.91, 6.92};
+        double t_hi = nr >= 1 ? us9[nr] : 0, t_lo = nr >= 2 ? us9[nr - 1] : 0;
+        if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
+            std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
         const int rs = nr >= 2 ? persist_rot_scratch(nr, h->cfg.mode) : -1;
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
-            plan_rotation(B, S, us9[nr], us9[nr - 1], h->rot_plan)) {
+            plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
             h->p_plan.clear();
             for (int j = 0; j < h->rot_plan.K; ++j) h->p_plan.push_back({0, nr, false, j});
         }
