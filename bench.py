@@ -361,8 +361,8 @@ def main():
     rows_per_gpu = U * model.fold_shape(args.frames, True, args.target, args.overlap)[0]
     if info:
         # dominant kernel = largest avg duration x launches
-        dom = max(info, key=lambda r: (r[3] if r[3] == r[3] else 0) * r[4])
-        name, by, fl, us, n = dom
+        dom_i = max(range(len(info)), key=lambda i: (info[i][3] if info[i][3] == info[i][3] else 0) * info[i][4])
+        name, by, fl, us, n = info[dom_i]
         us_rank = us
         if world > 1:  # the slowest rank's launch bounds the job: roofline on the max over ranks
             t = torch.tensor([us], device='cpu' if rehearse else dev, dtype=torch.float64)
@@ -383,10 +383,14 @@ def main():
                 'stages_us': {r[0]: round(r[3], 3) for r in info}}
         if name in ('persist', 'persist_wide'):
             # one launch per row batch runs all S steps; a row rotation runs
-            # the call's rows over K launches, S / K steps each on average
+            # the call's rows over K launches of S / K steps on average, the time-sliced wide plan
+            # (§3.0f) over launches of fewer steps: us_per_step is per step of a launch, and
+            # call_us_per_step the kind's whole time in the call per step of S
             rot = model.rot_info() if name == 'persist' else (0, 0, 0)
-            steps_launch = S / rot[0] if rot[0] else S
+            steps_launch = model.persist_steps(dom_i)
             roof['us_per_step'] = us / steps_launch
+            roof['call_us_per_step'] = us * n / S
+            roof['steps_per_launch'] = steps_launch
             if rot[0]:
                 roof['rotation'] = {'launches': rot[0], 'steps_per_launch_hi_rows': rot[1],
                                     'steps_per_launch_lo_rows': rot[2],

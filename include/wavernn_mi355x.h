@@ -239,9 +239,20 @@ int wrnn_debug_decide(uint64_t seed, uint32_t stream, uint32_t step, uint32_t fo
  * q-row group leaves empty; *launches = 0 when no rotation pays (tests). */
 int wrnn_debug_rot_plan(int rows, int seq_len, double us_hi, double us_lo, int* launches, int* n_hi,
                         int* n_lo, int* vmap, size_t capacity);
+/* Time-sliced wide launches for R fold rows of S steps, without a device: on
+ * success *launches = K > 0 (0 = the plan does not apply), per launch k rows_steps[2 k] = rows per
+ * group and rows_steps[2 k + 1] = steps (capacity >= 2 K), and vmap (capacity >= K * 8 * 16
+ * pairs, may be NULL) the (physical row, step offset) of virtual row v = g + 8 r at
+ * [(k * 128 + v) * 2], (-1, -1) beyond the launch's rows (tests). */
+int wrnn_debug_slice_plan(int rows, int seq_len, int* launches, int* rows_steps, size_t rs_capacity, int* vmap,
+                          size_t capacity);
 /* The rotation of the last persistent call: launches (0 = none), steps per launch of the q + 1 /
  * q-row groups. */
 int wrnn_rot_info(wrnn_handle* h, int* launches, int* n_hi, int* n_lo);
+/* Steps per launch, averaged over the launches of stage `stage` (wrnn_stage_info's index) of the
+ * last persistent call: the call's S for row batches, less for rotated / time-sliced launches
+ * (DESIGN.md §3.0e-f). */
+int wrnn_persist_steps(wrnn_handle* h, int stage, double* steps_per_launch);
 
 /* Host-side exhaustive check of the wide launch's exchange layout (kernels_persist_wide.hip,
  * csrc/wide_layout.h) for a group of `rows_per_group` rows (1..16): returns the number of

@@ -64,7 +64,8 @@ constexpr int WR_GROUP = WR_G + WR_SLOTS * 16 * kPH;
 // Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
 // the instruction's 16-bit immediate (beyond it each access would pin an address register).
 constexpr int WL_RI = 0;                         // RowInfo of the group's rows (6 words each)
-constexpr int WL_FAIL = WL_RI + 128;
+constexpr int WL_VM = WL_RI + 6 * kPWideRows;     // (physical row, step offset) of each row slot
+constexpr int WL_FAIL = WL_VM + 2 * kPWideRows;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
 constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
@@ -182,7 +183,10 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 }
 
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-template <bool DBG>
+// ROT: a time-sliced launch (PersistArgs::vmap): row slot r of group g is the
+//      virtual row v = g + 8 r, which a.vmap maps to (physical row, step offset); the launch runs
+//      steps [0, t1) of its rows (their steps off .. off + t1 - 1) and saves their state at the end
+template <bool ROT, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
     int* sreg = reinterpret_cast<int*>(lds + WL_REG);
@@ -207,10 +211,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     const int cn = tid >> 4, cul = tid & 15;
     const bool cell = tid < 16 * R;
     const int cu = 16 * w + cul;
-    const int crow = g0 + kPG * (cell ? cn : 0);
+    // (physical) row of this lane's cell; a time-sliced launch maps the virtual row
+    const int crow = ROT ? a.vmap[g0 + kPG * (cell ? cn : 0)].x : g0 + kPG * (cell ? cn : 0);
     // timeout site record (PC_WHERE): site << 28 | slot << 22 (| wave << 19, added by the poller);
     // the step goes to PC_WHERE + 2 whole
-    auto wh = [&](unsigned site) { return site << 28 | (unsigned)w << 22; };
+    // (recomputed per use from the scalar slot index: the hoisted constants held VGPRs)
+    auto wh = [&](unsigned site) {
+        unsigned ww = (unsigned)w;
+        asm volatile("" : "+s"(ww));
+        return site << 28 | ww << 22;
+    };
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * WX_GROUP);
     const bool trace = a.phases != nullptr;
     uint32_t* ph = trace ? a.phases + (size_t)(g * kPM + w) * kPPhases : nullptr;
@@ -249,7 +259,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         g2z = a.st_gh2[(size_t)crow * 3 * kPH + kPH + cu];
         g2n = a.st_gh2[(size_t)crow * 3 * kPH + 2 * kPH + cu];
     }
-    if (tid < R) reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid < R) {
+        reinterpret_cast<RowInfo*>(lds + WL_RI)[tid] = a.rows[g0 + kPG * tid];
+        reinterpret_cast<int2*>(lds + WL_VM)[tid] = ROT ? a.vmap[g0 + kPG * tid] : make_int2(g0 + kPG * tid, 0);
+    }
     if (tid == 0) lds[WL_FAIL] = 0.f;
     // biases of the slot in LDS: read per step by the epilogues (a global load there would
     // hold up the wave's next poll behind its latency)
@@ -356,14 +369,18 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     //  * the Gumbel noise of (tau, row, class u) in k_gumbel's fixed-point form (philox.h
     //    gumbel_q_of) -- no [S][B][n] noise stream either.
     auto ring_make = [&](int n, int u, int tau) {
-        const int tc = tau < a.S ? tau : a.S - 1;
+        // (a time-sliced row at offset off: its own steps end at S, its noise is drawn at its
+        // absolute step)
+        const int off = ROT ? reinterpret_cast<const int2*>(lds + WL_VM)[n].y : 0;
+        const int tc = tau < a.S - off ? tau : a.S - off - 1;
         int uu = u;
         asm volatile("" : "+v"(uu));
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
         const unsigned cell_i = (unsigned)((tau & 3) * 16 * kPH + n * kPH + uu);
         {
             // the noise of class u (a padding class beyond n_classes is drawn and never used)
-            const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+            const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)(tau + off), (uint32_t)ri.fold, ri.stream,
+                                       a.k0, a.k1);
             const uint32_t wd = (uu & 3) == 0 ? o.x : (uu & 3) == 1 ? o.y : (uu & 3) == 2 ? o.z : o.w;
             __builtin_amdgcn_raw_buffer_store_b32(gumbel_q_of(wd), rr, (unsigned)WR_G * 4u + cell_i * 4u, 0, 0);
         }
@@ -603,7 +620,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     float s;
                     psums(I1(), WL_PS, 1, &s);
                     const float lg = p_add(s, lds[WL_BIAS + 96 + cul]);
-                    p_dbg_logit<DBG>(a.dbg, t, crow, cu, a.B, a.n_classes, lg);
+                    p_dbg_logit<DBG>(a.dbg, t + (ROT ? reinterpret_cast<const int2*>(lds + WL_VM)[cn].y : 0), crow, cu,
+                                     a.B, a.n_classes, lg);
                     const CandKey k = cand_key(lg, __float_as_uint(pg), cu);
                     kh = k.hi;
                     kl = k.lo;
@@ -667,7 +685,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 if (w == 0 && cell && cul == 0) {
                     int nn = cn;
                     asm volatile("" : "+v"(nn));
-                    const unsigned ro = (unsigned)((g0 + kPG * nn) * a.ld);
+                    const int2 vm = reinterpret_cast<const int2*>(lds + WL_VM)[nn];
+                    const unsigned ro = (unsigned)(vm.x * a.ld + vm.y);
                     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels), ro * 2u,
                                                           (unsigned)t * 2u, 0);
                     bst(x, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -704,6 +723,21 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #undef WXSTAMP
 #undef WR
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+    // ---- the rows' state for a later launch (time-sliced or chunked calls): x1, h1 of step t1
+    // (GRU1 of the last step), h2 of step t1 - 1, gh2 = W_hh2 h2 + b_hh2 of the next GRU2 --
+    // k_persist's chunk-state layout
+    // (the row re-read from LDS: keeping crow live across the step loop cost a spilled register)
+    if ((ROT || a.t1 < a.S) && cell && lds[WL_FAIL] == 0.f) {
+        int nn = cn;
+        asm volatile("" : "+v"(nn));
+        const int row = reinterpret_cast<const int2*>(lds + WL_VM)[nn].x;
+        a.st_x1[(size_t)row * kPH + cu] = x1c;
+        a.st_h1[(size_t)row * kPH + cu] = h1r;
+        a.st_h2[(size_t)row * kPH + cu] = h2r;
+        a.st_gh2[(size_t)row * 3 * kPH + cu] = g2r;
+        a.st_gh2[(size_t)row * 3 * kPH + kPH + cu] = g2z;
+        a.st_gh2[(size_t)row * 3 * kPH + 2 * kPH + cu] = g2n;
+    }
 }
 
 size_t persist_wide_lds_bytes() { return (size_t)WL_TOTAL * sizeof(float); }
@@ -775,7 +809,12 @@ size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
 
 int persist_wide_scratch() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<false, false>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+int persist_wide_rot_scratch() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<true, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
@@ -783,8 +822,13 @@ hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
     if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > kPM * 16 ||
         a.mode != 0 || a.wwide == nullptr || a.wring == nullptr)
         return hipErrorInvalidValue;
-    if (a.dbg.out) return persist_launch<k_persist_wide<true>>(persist_wide_lds_bytes(), a, s);
-    return persist_launch<k_persist_wide<false>>(persist_wide_lds_bytes(), a, s);
+    if (a.vmap) {
+        if (a.p1q == nullptr) return hipErrorInvalidValue;  // time-sliced rows: P1 formed in-kernel
+        if (a.dbg.out) return persist_launch<k_persist_wide<true, true>>(persist_wide_lds_bytes(), a, s);
+        return persist_launch<k_persist_wide<true, false>>(persist_wide_lds_bytes(), a, s);
+    }
+    if (a.dbg.out) return persist_launch<k_persist_wide<false, true>>(persist_wide_lds_bytes(), a, s);
+    return persist_launch<k_persist_wide<false, false>>(persist_wide_lds_bytes(), a, s);
 }
 
 }  // namespace wrnn

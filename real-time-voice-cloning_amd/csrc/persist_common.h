@@ -173,7 +173,9 @@ __device__ __forceinline__ void p_dbg_logit(const DbgLogits& d, int t, int row, 
                                             int n, float l) {
     if constexpr (!DBG) return;
     if (d.out == nullptr) return;
-    const int k = __builtin_amdgcn_readfirstlane(d.map[t]);
+    // (per lane: the lanes of one wave can hold rows at different step offsets -- a time-sliced
+    // wide launch)
+    const int k = d.map[t];
     if (k >= 0) d.out[((size_t)k * B + row) * n + cls] = l;
 }
 

@@ -232,6 +232,13 @@ struct wrnn_handle {
         std::vector<int2> vmap;     // [K][kPG * nr_hi]
         std::vector<int> gnr, git;  // [K][kPG]
     } rot_plan;
+    // Time-sliced wide launches of the last call: per launch the rows per group,
+    // the steps and the virtual-row map (physical row, step offset), by virtual row g + 8 r
+    struct WLaunch {
+        int nr, steps;
+        std::vector<int2> vmap;  // [kPG * nr]
+    };
+    std::vector<WLaunch> wrot;
     std::vector<PLaunch> p_plan;    // PERSIST: the launches of the last call, in order
     std::vector<int> pev_kind;      // per timed launch: 1 wide, 0 otherwise
     std::vector<int> pev_rows;      // per timed launch: rows (8 nr)
@@ -245,6 +252,7 @@ struct wrnn_handle {
         int wide;
         double rows;       // real rows summed over the kind's launches
         int launches;
+        double steps = 0, row_steps = 0;  // steps / real row-steps summed over the kind's launches
     };
     std::vector<PStage> pstages;  // launch kinds of the last PERSIST call
     double p_avg_steps = 0;                      // steps per timed launch
@@ -1876,6 +1884,54 @@ bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan&
     return true;
 }
 
+// Time-sliced wide launches. The wide kernel's step costs nearly the same for
+// any row count up to 16 per group (MFMA tiles of 16 columns), so R = 8 R_g rows with
+// 16 < R_g <= 32 run best as launches of 16 rows per group over rotating row sets: with
+// d = R_g - 16 rows of each group idle per launch (a circular shift by gcd(R_g, d) rows per
+// launch), K = R_g / gcd launches make every row active in A = 16 K / R_g of them; each runs
+// n = S / A steps (integer part), and ceil(R_g / 16) short launches give every row the remaining
+// S - A n. C4 (144 rows, 18 per group): 9 launches of 1,512 steps + 2 of 4 -- 1.125 S wide steps
+// instead of S wide steps + S steps of a 2-row register-resident launch for the 16 rows left over.
+bool plan_wide_slices(int R, int S, std::vector<wrnn_handle::WLaunch>& out) {
+    out.clear();
+    if (R % kPG) return false;
+    const int Rg = R / kPG;
+    if (Rg <= kPWideRows || Rg > 2 * kPWideRows) return false;
+    const int d = Rg - kPWideRows, gg = gcd_i(Rg, d), K = Rg / gg, A = kPWideRows * K / Rg;
+    const int n = S / A, rem = S - A * n;
+    if (n < 64) return false;
+    std::vector<int> off(R, 0);
+    for (int j = 0; j < K; ++j) {
+        std::vector<char> idle(Rg, 0);
+        for (int k = 0; k < d; ++k) idle[(j * gg + k) % Rg] = 1;
+        wrnn_handle::WLaunch L{kPWideRows, n, std::vector<int2>((size_t)kPG * kPWideRows)};
+        for (int g = 0; g < kPG; ++g) {
+            int r = 0;
+            for (int i = 0; i < Rg; ++i)
+                if (!idle[i]) {
+                    const int row = g + kPG * i;
+                    L.vmap[(size_t)g + kPG * r++] = make_int2(row, off[row]);
+                    off[row] += n;
+                }
+        }
+        out.push_back(std::move(L));
+    }
+    for (int k = 0; rem > 0 && k * kPWideRows < Rg; ++k) {  // the remaining steps of every row
+        const int nr = std::min(kPWideRows, Rg - k * kPWideRows);
+        wrnn_handle::WLaunch L{nr, rem, std::vector<int2>((size_t)kPG * nr)};
+        for (int g = 0; g < kPG; ++g)
+            for (int r = 0; r < nr; ++r) {
+                const int row = g + kPG * (k * kPWideRows + r);
+                L.vmap[(size_t)g + kPG * r] = make_int2(row, off[row]);
+                off[row] += rem;
+            }
+        out.push_back(std::move(L));
+    }
+    for (int r = 0; r < R; ++r)
+        if (off[r] != S) return (out.clear(), false);
+    return true;
+}
+
 // PERSIST engine: P1 for all steps (one MFMA GEMM), Gumbel noise (RAW), step-0 state, then
 // the persistent recurrence in chunks (one chunk per call unless a progress callback wants
 // reports; every 1000 steps then).
@@ -2109,24 +2165,35 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     // row rotation: per launch j the virtual-row map, rows / steps per group and the RowInfo
     // table by virtual row (rel0 advanced by the row's offset), one device block per launch
     const auto& RP = h->rot_plan;
+    // (register-resident rotation or time-sliced wide launches): per launch j the virtual-row map,
+    // for the rotation the rows and steps per group, and the RowInfo table by virtual row (rel0
+    // advanced by the row's offset) -- one device block per launch
     const bool rotp = nb > 0 && h->p_plan[0].rot >= 0;
-    size_t rot_stride = 0;
+    std::vector<size_t> rot_off;  // per launch: byte offset of its block
     if (rotp) {
-        const int nv = kPG * RP.nr_hi;
-        const size_t o_gnr = (size_t)nv * sizeof(int2), o_git = o_gnr + kPG * sizeof(int),
-                     o_rows = o_git + kPG * sizeof(int);
-        rot_stride = (o_rows + (size_t)nv * sizeof(RowInfo) + 255) & ~(size_t)255;
-        h->rot_host.assign(rot_stride * RP.K, 0);
-        for (int j = 0; j < RP.K; ++j) {
-            char* base = h->rot_host.data() + rot_stride * j;
-            std::memcpy(base, &RP.vmap[(size_t)j * nv], (size_t)nv * sizeof(int2));
-            std::memcpy(base + o_gnr, &RP.gnr[(size_t)j * kPG], kPG * sizeof(int));
-            std::memcpy(base + o_git, &RP.git[(size_t)j * kPG], kPG * sizeof(int));
-            RowInfo* rv = reinterpret_cast<RowInfo*>(base + o_rows);
+        auto nv_of = [&](const wrnn_handle::PLaunch& L) { return kPG * (L.wide ? h->wrot[L.rot].nr : RP.nr_hi); };
+        size_t total = 0;
+        for (const auto& L : h->p_plan) {
+            rot_off.push_back(total);
+            const int nv = nv_of(L);
+            total += ((size_t)nv * (sizeof(int2) + sizeof(RowInfo)) + 2 * kPG * sizeof(int) + 255) & ~(size_t)255;
+        }
+        h->rot_host.assign(total, 0);
+        for (int b = 0; b < nb; ++b) {
+            const auto& L = h->p_plan[b];
+            const int nv = nv_of(L);
+            char* base = h->rot_host.data() + rot_off[b];
+            const int2* vm = L.wide ? h->wrot[L.rot].vmap.data() : &RP.vmap[(size_t)L.rot * nv];
+            std::memcpy(base, vm, (size_t)nv * sizeof(int2));
+            int* gi = reinterpret_cast<int*>(base + (size_t)nv * sizeof(int2));
+            if (!L.wide) {
+                std::memcpy(gi, &RP.gnr[(size_t)L.rot * kPG], kPG * sizeof(int));
+                std::memcpy(gi + kPG, &RP.git[(size_t)L.rot * kPG], kPG * sizeof(int));
+            }
+            RowInfo* rv = reinterpret_cast<RowInfo*>(gi + 2 * kPG);
             for (int v = 0; v < nv; ++v) {
-                const int2 m = RP.vmap[(size_t)j * nv + v];
-                rv[v] = h->rows_host[m.x];
-                rv[v].rel0 += m.y;
+                rv[v] = h->rows_host[vm[v].x];
+                rv[v].rel0 += vm[v].y;
             }
         }
         CHECK(P.rot.alloc(h->rot_host.size()));
@@ -2143,14 +2210,21 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         a.vmap = nullptr;
         a.gnr = a.giters = nullptr;
         a.rows = (const RowInfo*)ws.rows.p;
+        double steps_b = S;  // (this launch's steps, for the per-launch accounting)
         if (L.rot >= 0) {
-            const char* base = (const char*)P.rot.p + rot_stride * L.rot;
-            const int nv = kPG * RP.nr_hi;
+            const char* base = (const char*)P.rot.p + rot_off[b];
+            const int nv = kPG * L.nr;
             a.vmap = (const int2*)base;
-            a.gnr = (const int*)(base + (size_t)nv * sizeof(int2));
-            a.giters = a.gnr + kPG;
             a.rows = (const RowInfo*)(base + (size_t)nv * sizeof(int2) + 2 * kPG * sizeof(int));
-            a.t1 = std::max(RP.n_hi, RP.n_lo);
+            if (L.wide) {
+                a.t1 = h->wrot[L.rot].steps;
+                steps_b = a.t1;
+            } else {
+                a.gnr = (const int*)(base + (size_t)nv * sizeof(int2));
+                a.giters = a.gnr + kPG;
+                a.t1 = std::max(RP.n_hi, RP.n_lo);
+                steps_b = (double)S / RP.K;  // (per launch, on average: S per call)
+            }
         }
         if (L.wide)  // sentinel-initialised vector slots (kernels_persist_wide*.hip polls)
             HIPC(rr ? persist_wide_rr_reset_xbuf(P.xbuf.f(), st) : persist_wide_reset_xbuf(P.xbuf.f(), st));
@@ -2166,7 +2240,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             HIPC(hipEventCreate(&e1));
             h->pev.push_back(e0);
             h->pev.push_back(e1);
-            h->pev_steps.push_back(L.rot >= 0 ? (double)S / RP.K : (double)S);  // (rotation: S per call)
+            h->pev_steps.push_back(steps_b);
             h->pev_kind.push_back(L.wide ? 1 : 0);
             h->pev_rows.push_back(kPG * L.nr);
             HIPC(hipEventRecord(e0, st));
@@ -2303,7 +2377,13 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     h->p_macs = macs;
     h->pstages.clear();
     for (const auto& L : h->p_plan) {
-        const int real = std::max(0, std::min(B, L.rb + kPG * L.nr) - L.rb);
+        int real = std::max(0, std::min(B, L.rb + kPG * L.nr) - L.rb);
+        double steps = S;
+        if (L.rot >= 0 && L.wide) steps = h->wrot[L.rot].steps;  // time-sliced: nr rows per group
+        else if (L.rot >= 0) {                                    // rotation: all rows, S / K steps
+            real = B;
+            steps = (double)S / h->rot_plan.K;
+        }
         const char* nm = L.wide ? "persist_wide" : "persist";
         auto it = std::find_if(h->pstages.begin(), h->pstages.end(),
                                [&](const wrnn_handle::PStage& q) { return q.name == nm; });
@@ -2313,6 +2393,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         }
         it->rows += real;
         it->launches += 1;
+        it->steps += steps;
+        it->row_steps += steps * real;
     }
     return WRNN_OK;
 }
@@ -2425,6 +2507,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // below), e.g. 9-bit: 18 rows -> one launch at 3 rows; 144 rows -> one wide launch of 128
     // rows + one launch at 2 rows.
     std::vector<wrnn_handle::PLaunch> lplan;
+    double plan_us = 0;  // the plan's summed per-step cost (us), for the time-sliced alternative
     if (h->pw.ok) {
         struct Opt {
             int nr;
@@ -2502,9 +2585,30 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                 rb += kPG * o.nr;
                 r = std::max(0, r - kPG * o.nr);
             }
+            plan_us = best[B];
         }
     }
-    const int Bplan = lplan.empty() ? B : lplan.back().rb + kPG * lplan.back().nr;
+    // time-sliced wide launches (plan_wide_slices), when cheaper than the plan
+    // above by the same cost model (fatchord RAW <= 512 classes with the in-kernel P1 ring;
+    // WRNN_PERSIST_SLICE=0 or WRNN_PERSIST_WIDE=0: off)
+    h->wrot.clear();
+    if (h->pw.ok && !h->pw.gen && !h->pw.rr && h->pw.wwide && h->cfg.mode == WRNN_MODE_RAW && p1_ring_ok(h) &&
+        !lplan.empty()) {
+        const char* e1 = std::getenv("WRNN_PERSIST_SLICE");
+        const char* e2 = std::getenv("WRNN_PERSIST_WIDE");
+        std::vector<wrnn_handle::WLaunch> sl;
+        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && persist_wide_rot_scratch() == 0 &&
+            plan_wide_slices(B, S, sl)) {
+            double cost = 60.0 * (sl.size() - 1);  // (an extra launch: weights, ring prologue)
+            for (const auto& L : sl) cost += L.steps * (10.5 + 0.055 * L.nr);
+            if (cost < 0.98 * plan_us * S) {
+                lplan.clear();
+                for (int j = 0; j < (int)sl.size(); ++j) lplan.push_back({0, sl[j].nr, true, j});
+                h->wrot = std::move(sl);
+            }
+        }
+    }
+    const int Bplan = lplan.empty() ? B : !h->wrot.empty() ? B : lplan.back().rb + kPG * lplan.back().nr;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
         if (!h->pw.ok)
@@ -3009,10 +3113,11 @@ int wrnn_stage_info(wrnn_handle* h, int stage, char* name, size_t name_cap, doub
         if (name && name_cap) std::snprintf(name, name_cap, "%s", q.name.c_str());
         // per launch = steps x (recurrent weights once per step + the launch's real rows x
         // per-row-step stream) / FLOPs
-        const double steps = h->p_avg_steps > 0 ? h->p_avg_steps : h->last_S;
-        const double rows = q.launches ? q.rows / q.launches : 0.0;
-        if (bytes) *bytes = steps * (h->p_wbytes + rows * h->p_row_bytes);
-        if (flops) *flops = steps * 2.0 * h->p_macs * rows;
+        // (summed over the kind's launches, per launch: launches of different steps and rows --
+        // the time-sliced wide plan -- are counted each with its own)
+        const double nl = q.launches ? q.launches : 1.0;
+        if (bytes) *bytes = (q.steps * h->p_wbytes + q.row_steps * h->p_row_bytes) / nl;
+        if (flops) *flops = q.row_steps * 2.0 * h->p_macs / nl;
         return WRNN_OK;
     }
     if (n_stages) *n_stages = (int)h->stages.size();
@@ -3079,9 +3184,42 @@ int wrnn_debug_rot_plan(int rows, int seq_len, double us_hi, double us_lo, int* 
     return WRNN_OK;
 }
 
+int wrnn_persist_steps(wrnn_handle* h, int stage, double* steps_per_launch) {
+    if (!h || !steps_per_launch) return fail(WRNN_ERR_INVALID, "null argument");
+    if (h->last_engine != WRNN_ENGINE_PERSIST || stage < 0 || stage >= (int)h->pstages.size())
+        return fail(WRNN_ERR_INVALID, "bad stage index");
+    const auto& q = h->pstages[stage];
+    *steps_per_launch = q.launches ? q.steps / q.launches : 0.0;
+    return WRNN_OK;
+}
+
+int wrnn_debug_slice_plan(int rows, int seq_len, int* launches, int* rows_steps, size_t rs_capacity, int* vmap,
+                          size_t capacity) {
+    if (!launches || !rows_steps) return fail(WRNN_ERR_INVALID, "null argument");
+    if (rows < 1 || seq_len < 1) return fail(WRNN_ERR_INVALID, "bad arguments");
+    std::vector<wrnn_handle::WLaunch> sl;
+    *launches = 0;
+    if (!plan_wide_slices(rows, seq_len, sl)) return WRNN_OK;
+    const int K = (int)sl.size(), nv = kPG * kPWideRows;
+    if (rs_capacity < 2 * (size_t)K || (vmap && capacity < (size_t)K * nv * 2)) return fail(WRNN_ERR_CAPACITY, "capacity");
+    for (int k = 0; k < K; ++k) {
+        rows_steps[2 * k] = sl[k].nr;
+        rows_steps[2 * k + 1] = sl[k].steps;
+        if (vmap)
+            for (int v = 0; v < nv; ++v) {
+                const bool used = v < kPG * sl[k].nr;
+                vmap[((size_t)k * nv + v) * 2] = used ? sl[k].vmap[v].x : -1;
+                vmap[((size_t)k * nv + v) * 2 + 1] = used ? sl[k].vmap[v].y : -1;
+            }
+    }
+    *launches = K;
+    return WRNN_OK;
+}
+
 int wrnn_rot_info(wrnn_handle* h, int* launches, int* n_hi, int* n_lo) {
     if (!h || !launches || !n_hi || !n_lo) return fail(WRNN_ERR_INVALID, "null argument");
-    const bool rot = !h->p_plan.empty() && h->p_plan[0].rot >= 0 && h->last_engine == WRNN_ENGINE_PERSIST;
+    const bool rot = !h->p_plan.empty() && h->p_plan[0].rot >= 0 && !h->p_plan[0].wide &&
+                     h->last_engine == WRNN_ENGINE_PERSIST;
     *launches = rot ? h->rot_plan.K : 0;
     *n_hi = rot ? h->rot_plan.n_hi : 0;
     *n_lo = rot ? h->rot_plan.n_lo : 0;

@@ -261,6 +261,7 @@ size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
 int persist_wide_scratch();
+int persist_wide_rot_scratch();  // the time-sliced instance (PersistArgs::vmap)
 int wide_layout_check(int rows_per_group);  // host: violations of the exchange layout (wide_layout.h)
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise

@@ -38,7 +38,7 @@ EXPORTED = [
     'wrnn_stage_timing', 'wrnn_stage_info', 'wrnn_debug_noise', 'wrnn_debug_upsample',
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
-    'wrnn_debug_beta', 'wrnn_debug_decide', 'wrnn_debug_rot_plan', 'wrnn_rot_info', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
+    'wrnn_debug_beta', 'wrnn_debug_decide', 'wrnn_debug_rot_plan', 'wrnn_debug_slice_plan', 'wrnn_rot_info', 'wrnn_persist_steps', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
     'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits', 'wrnn_debug_wide_layout',
 ]
 
@@ -136,6 +136,8 @@ def load_library(path=None):
         'wrnn_debug_rot_plan': (c_int, [c_int, c_int, ctypes.c_double, ctypes.c_double, P(c_int), P(c_int),
                                         P(c_int), P(c_int), c_size_t]),
         'wrnn_rot_info': (c_int, [c_void_p, P(c_int), P(c_int), P(c_int)]),
+        'wrnn_debug_slice_plan': (c_int, [c_int, c_int, P(c_int), P(c_int), c_size_t, P(c_int), c_size_t]),
+        'wrnn_persist_steps': (c_int, [c_void_p, c_int, P(ctypes.c_double)]),
         'wrnn_debug_decide': (c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, P(ctypes.c_float), c_int, P(c_int),
                                       P(ctypes.c_double)]),

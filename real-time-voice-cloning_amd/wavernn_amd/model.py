@@ -221,6 +221,12 @@ class WaveRNN:
         _abi.check(self._lib.wrnn_rot_info(self._h, ctypes.byref(k), ctypes.byref(nh), ctypes.byref(nl)))
         return k.value, nh.value, nl.value
 
+    def persist_steps(self, stage):
+        """Steps per launch of persistent stage `stage` (stage_info order) of the last call."""
+        v = ctypes.c_double()
+        _abi.check(self._lib.wrnn_persist_steps(self._h, int(stage), ctypes.byref(v)))
+        return v.value
+
     def fallback_info(self):
         """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
         n = ctypes.c_int()

@@ -44,7 +44,14 @@ def test_c2_fatchord_is_rotated_over_three_launches(mode, monkeypatch):
     assert _run('fatchord-wavernn', mode, 9, 1) == [(0, 3, False)]
 
 
-def test_c4_shape_is_one_wide_launch_and_one_of_2_rows():
+def test_c4_shape_is_time_sliced_over_wide_launches(monkeypatch):
+    """C4 per GPU (144 rows, 18 per group): time-sliced wide launches -- 9 of
+    16 rows per group x 1,512 steps, then the last 4 steps in launches of 16 and 2 rows per
+    group; WRNN_PERSIST_SLICE=0 restores one wide launch of 128 rows + one register-resident
+    launch of 2 rows per group."""
+    plan = _run('fatchord-wavernn', 'RAW', 9, 8)
+    assert plan == [(0, 16, True)] * 10 + [(0, 2, True)], plan
+    monkeypatch.setenv('WRNN_PERSIST_SLICE', '0')
     plan = _run('fatchord-wavernn', 'RAW', 9, 8)
     assert sorted((nr, wide) for _, nr, wide in plan) == [(2, False), (16, True)]
     assert sum(8 * nr for _, nr, _ in plan) == 144

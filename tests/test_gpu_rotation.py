@@ -1,4 +1,4 @@
-"""Row rotation of the persistent engine on the GPU: a call whose rows leave the
+"""Row rotation and time-sliced wide launches (§3.0f) on the GPU: a call whose rows leave the
 XCD groups uneven (R % 8 != 0) runs as K launches over rotating row sets, groups of q rows on
 their own q-row body. The rotation only moves WHERE and WHEN a row's steps run: every row's
 arithmetic is the same, so the labels / samples must equal the single-launch plan's
@@ -104,3 +104,45 @@ def test_rotated_call_reports_progress_at_the_reference_cadence(monkeypatch):
     assert all(n == S and b == 18 for _, n, b in seen)
     b_, rb, _ = _call(m, mel, monkeypatch, rot=False)
     assert np.array_equal(a, b_)
+
+
+def test_time_sliced_wide_equals_wide_plus_tail(monkeypatch):
+    """8 utterances x 18 rows (the C4 shape at 4,800 steps): the time-sliced wide launches (every
+    row through 16-row-per-group wide launches at its own offsets, state across launches) give
+    the labels of the wide 128-row launch + register-resident 16-row launch plan
+    (WRNN_PERSIST_SLICE=0) bit for bit, and so do the wide rows' logits recorded around the slice
+    boundaries (600 steps per launch at 4,800 steps: 8 of 9 launches per row)."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    T = _frames_for(m, 18)
+    devs = [torch.from_numpy((synth_mel(T, 40 + u) / sp.max_abs_value).astype(np.float32)).cuda() for u in range(8)]
+    steps = [0, 599, 600, 601, 1199, 1200, 2400, 4799]
+    res = {}
+    for sl in ('1', '0'):
+        monkeypatch.setenv('WRNN_PERSIST_SLICE', sl)
+        m.set_seed(9)
+        m.set_debug_steps(steps)
+        try:
+            out, roff, S = m.generate_batch_device(devs, True, TARGET, OVERLAP)
+            lab = out.cpu().numpy()
+            logs = {s: m.debug_logits(s, range(lab.shape[0])) for s in steps}
+        finally:
+            m.set_debug_steps(None)
+        res[sl] = (lab, logs, m.plan_info())
+    (a, la, pa), (b, lb, pb) = res['1'], res['0']
+    assert len(pa) > 2 and all(w for _, _, w in pa) and any(not w for _, _, w in pb), (pa, pb)
+    d = np.argwhere(a != b)
+    assert len(d) == 0, f'first difference (row, step) {d[np.argmin(d[:, 1])].tolist()}'
+    # (logits: the rows both plans run on the wide kernel -- the other plan's 16 register-resident
+    # rows, wherever its launch order puts them, run a different fp32 summation order)
+    wide = np.concatenate([np.arange(rb, rb + 8 * nr) for rb, nr, w in pb if w])
+    assert len(wide) == 128
+    bad = []
+    for s in steps:
+        dr = [int(r) for r in wide if not np.array_equal(la[s][r], lb[s][r])]
+        if dr:
+            dd = np.abs(la[s][dr] - lb[s][dr])
+            bad.append((s, len(dr), dr[:20], float(dd.max()), int((dd > 0).sum())))
+    assert not bad, (bad, pa, pb)

@@ -70,3 +70,48 @@ def test_no_rotation_where_it_cannot_pay(R):
     assert lib.wrnn_debug_rot_plan(R, 12100, t_hi, t_lo, ctypes.byref(k), ctypes.byref(nh), ctypes.byref(nl),
                                    None, 0) == 0
     assert k.value == 0
+
+
+def slice_plan(R, S=12100):
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    k = ctypes.c_int()
+    rs = (ctypes.c_int * 128)()
+    vm = (ctypes.c_int * (64 * 128 * 2))()
+    assert lib.wrnn_debug_slice_plan(R, S, ctypes.byref(k), rs, 128, vm, 64 * 128 * 2) == 0
+    K = k.value
+    return K, np.array(rs[:2 * K]).reshape(K, 2), np.array(vm[:K * 128 * 2]).reshape(K, 16, 8, 2)
+
+
+@pytest.mark.parametrize('R', [136, 144, 160, 192, 256])
+def test_wide_time_slices_plan_invariants(R):
+    """Time-sliced wide launches: at most 16 rows per group and launch, every
+    row at most once per launch and in its own group (rows g + 8 i), offsets advanced by the
+    launch's steps, every row at exactly S. C4 (144 rows): 9 launches of 1,512 steps at 16 rows
+    per group, then 2 of the remaining 4 steps (16 and 2 rows per group)."""
+    S = 12100
+    K, rs, vm = slice_plan(R, S)
+    assert K > 1
+    off = np.zeros(R, int)
+    for k in range(K):
+        nr, steps = rs[k]
+        assert 1 <= nr <= 16 and steps >= 1
+        rows = []
+        for g in range(8):
+            for r in range(16):
+                row, o = vm[k, r, g]
+                if r >= nr:
+                    assert (row, o) == (-1, -1)
+                    continue
+                assert row % 8 == g and o == off[row], (k, g, r, row, o, off[row])
+                rows.append(row)
+        assert len(rows) == len(set(rows)) == 8 * nr
+        off[rows] += steps
+    assert (off == S).all()
+    if R == 144:
+        assert K == 11 and rs[:9].tolist() == [[16, 1512]] * 9 and rs[9:].tolist() == [[16, 4], [2, 4]]
+
+
+@pytest.mark.parametrize('R', [128, 120, 143, 264, 18])
+def test_wide_time_slices_only_between_16_and_32_rows_per_group(R):
+    assert slice_plan(R)[0] == 0

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out/rot
 for r in 1 2; do
-  for rates in "5.91,5.15" "5.91,5.22" "5.91,5.08" "5.95,5.15"; do
+  for rates in ${RATES:-"5.91,5.22" "5.91,5.28" "5.91,5.35" "5.91,5.42"}; do
     WRNN_ROT_US=$rates timeout -k 10 120 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/rot/$rates.r$r.log 2>&1 || { echo "fail $rates"; exit 1; }
     python - gpurun_out/rot/$rates.r$r.log "$rates" <<'PY'
 import json,sys
