@@ -53,13 +53,6 @@ using wide::WX_GROUP;
 constexpr unsigned kSent = 0x7fbadbadu;  // a signalling NaN: no arithmetic result is ever this
 enum WBuf : int { WB_X1 = 0, WB_H1, WB_X2, WB_H2, WB_Y1, WB_Y2, WB_N };
 static_assert(WB_N == wide::kBufs, "one slot pair per published vector");
-// Per-group operand ring (PersistArgs::wring, runtime.hip persist_wide_ring_floats): P1 (r, z, n of
-// W_ih1 (I c) + b_ih1, then I c + b_I) and the Gumbel noise of every cell for 4 steps,
-// [slot = step & 3][row n][unit / class], formed in-kernel three steps ahead (see the fc3 window)
-constexpr int WR_SLOTS = 4;
-constexpr int WR_G = WR_SLOTS * 16 * kPH * 4;  // P1: float4 [4][16][512] at 0; noise: float [4][16][512]
-constexpr int WR_GROUP = WR_G + WR_SLOTS * 16 * kPH;
-
 // ---- LDS (floats) -------------------------------------------------------------------------
 // Everything read per step sits in the first 64 KiB so every ds_read / ds_write offset fits
 // the instruction's 16-bit immediate (beyond it each access would pin an address register).
@@ -67,14 +60,16 @@ constexpr int WL_RI = 0;                         // RowInfo of the group's rows 
 constexpr int WL_VM = WL_RI + 6 * kPWideRows;     // (physical row, step offset) of each row slot
 constexpr int WL_FAIL = WL_VM + 2 * kPWideRows;
 constexpr int WL_REG = WL_FAIL + 4;              // group, slot, registration result (ints)
-constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16] of the slot
+constexpr int WL_BIAS = WL_REG + 4;              // b_hh1 [3][16], b_hh2 [3][16], b_fc3 [16 (+16)] of the slot
+constexpr int WL_P1R = 512;                      // P1 ring: float4 [16 n][16 j] (one slot, p1_make)
+constexpr int WL_GR = WL_P1R + 16 * 16 * 4;      // noise ring: [16 n][16 (C10: 32)] (one slot, noise_make)
 constexpr int WL_PS = 2048;                      // 1-tile partials [8 v][16 n][16 o]
 constexpr int WL_PA = WL_PS + 8 * 256;           // 3-tile partials [8 v][3][16 n][16 o]
 constexpr int WL_PH = WL_PA + 8 * 3 * 256;       // W_hh1 h1 partials (same layout)
 constexpr int WL_HH2 = WL_PH + 8 * 3 * 256;      // W_hh2 r, z, n tiles: [3][8 v][4 q][64 l][4]
 constexpr int WL_HH2_SZ = 3 * 8 * 16 * 64;
 constexpr int WL_TOTAL = WL_HH2 + WL_HH2_SZ;
-static_assert(WL_BIAS + 112 <= 256, "small LDS arrays overflow their 1 KiB");
+static_assert(WL_BIAS + 128 <= WL_P1R && WL_GR + 16 * 32 <= WL_PS, "small LDS arrays overflow their region");
 static_assert(WL_HH2 * 4 <= 65536, "per-step LDS arrays must fit the 16-bit ds offset");
 static_assert(WL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB (no static LDS)");
 static_assert(sizeof(RowInfo) == 24, "RowInfo is 6 words");
@@ -171,7 +166,10 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 #pragma unroll
                 for (int i = 0; i < 4; ++i) mok &= p_ready(cc[i]);
                 const bool mbad = !__all(mok);
-                if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | ((threadIdx.x >> 6) << 19)) == 0u) {
+                // (the wave index read back as a scalar: a per-lane form was precomputed per site
+                // before the step loop and held VGPRs)
+                const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+                if ((threadIdx.x & 63) == 0 && atomicCAS(ctl + PC_WHERE, 0u, where | (wv << 19)) == 0u) {
                     ctl[PC_WHERE + 1] = mbad ? 1u : 0u;
                     ctl[PC_WHERE + 2] = step;
                 }
@@ -186,7 +184,12 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 // ROT: a time-sliced launch (PersistArgs::vmap): row slot r of group g is the
 //      virtual row v = g + 8 r, which a.vmap maps to (physical row, step offset); the launch runs
 //      steps [0, t1) of its rows (their steps off .. off + t1 - 1) and saves their state at the end
-template <bool ROT, bool DBG>
+// C10: up to 1024 classes (fatchord's 10-bit default): slot w also owns classes 512 + 16 w ..
+//      512 + 16 w + 15, a second fc3 tile whose A operands (a.wfc3b, 1 MiB per group image,
+//      L2-resident) are loaded every step in the hop-C wait -- the registers hold the other nine
+//      tiles; its partials go to PH after one more barrier (the gh1 / gh2 partial sums are read
+//      in the hop-C wait instead of hop D, so PH is free by then)
+template <bool ROT, bool C10, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
     int* sreg = reinterpret_cast<int*>(lds + WL_REG);
@@ -266,11 +269,12 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     if (tid == 0) lds[WL_FAIL] = 0.f;
     // biases of the slot in LDS: read per step by the epilogues (a global load there would
     // hold up the wave's next poll behind its latency)
-    if (tid < 112) {
+    if (tid < (C10 ? 128 : 112)) {
         const int k = tid < 96 ? tid % 48 : tid - 96;
         const float* src = tid < 48 ? a.b_hh1 : tid < 96 ? a.b_hh2 : a.b_fc3;
-        const int idx = tid < 96 ? (k / 16) * kPH + 16 * w + (k & 15) : 16 * w + k;
-        lds[WL_BIAS + tid] = tid >= 96 && 16 * w + k >= a.n_classes ? 0.f : src[idx];
+        const int cls = 16 * w + (k & 15) + (k >= 16 ? kPH : 0);  // (fc3: tile a, then tile b)
+        const int idx = tid < 96 ? (k / 16) * kPH + 16 * w + (k & 15) : cls;
+        lds[WL_BIAS + tid] = tid >= 96 && cls >= a.n_classes ? 0.f : src[idx];
     }
     // byte offsets in a slot: this lane's packet 0 (consumer); the packet of the unit quad
     // cul .. cul + 3 of row cn (producer: lane cul % 4 == 0 of the quad gathers and publishes;
@@ -323,16 +327,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     using I1 = std::integral_constant<int, 1>;
     using I3 = std::integral_constant<int, 3>;
     const rsrc_t fcr = mk_rsrc(a.fcond);
-    const rsrc_t rr = mk_rsrc(a.wring + (size_t)g * WR_GROUP);  // this group's operand ring
-    // per-step operands of the cell (L2-resident: the per-frame tables and the ring), loaded
-    // right after the hop E poll:
+    constexpr int NC = C10 ? 32 : 16;  // noise classes per row and slot in the LDS ring
+    // per-step operands of the cell, loaded right after the hop E poll (L2-resident per-frame
+    // tables):
     //   pc[0..2] GRU2 cond (W_ih2[:, 512:] a2 + b_ih2), pc[3] fc1 cond, pc[4] fc2 cond (frame t)
     // and right after the hop C poll (live only from fc3 to GRU1: fewer registers held over the
     // step's products):
-    //   pg       Gumbel noise of (row, class cu) at step t        (ring slot t & 3)
-    //   pp       P1(t + 1) of (row, unit cu), consumed by GRU1     (ring slot (t + 1) & 3)
+    //   pg (pg2) Gumbel noise of (row, class cu (512 + cu)) at step t (LDS ring, WL_GR)
+    //   pp       P1(t + 1) of (row, unit cu), consumed by GRU1          (LDS ring, WL_P1R)
     //   pv       v = W_ih1 w0 (r, z, n) and w0 of unit cu         (constants, L1-resident)
-    float pc[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, pg = 0.f;
+    float pc[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, pg = 0.f, pg2 = 0.f;
     float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), pv = make_float4(0.f, 0.f, 0.f, 0.f);
     auto prefetch = [&](int t) {
         if (!cell) return;
@@ -347,44 +351,56 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         pc[4] = bld(fcr, fo + (unsigned)(a.oF2 + uu) * 4u, 0);
     };
     const rsrc_t vr = mk_rsrc(a.v), w0r = mk_rsrc(a.w0);
-    auto prefetch_d = [&](int t) {
+    auto prefetch_d = [&]() {
         if (!cell) return;
         int uu = cu;
         asm volatile("" : "+v"(uu));
-        const unsigned cell_i = (unsigned)(cn * kPH + (uu & (kPH - 1)));
-        pg = bld(rr, (unsigned)WR_G * 4u + ((unsigned)(t & 3) * 16u * kPH + cell_i) * 4u, 0);
-        pp = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rr, ((unsigned)((t + 1) & 3) * 16u * kPH + cell_i) * 16u, 0, 0));
+        pg = lds[WL_GR + cn * NC + cul];
+        if constexpr (C10) pg2 = lds[WL_GR + cn * NC + 16 + cul];
+        pp = reinterpret_cast<const float4*>(lds + WL_P1R)[cn * 16 + cul];
         pv.x = bld(vr, (unsigned)uu * 4u, 0);
         pv.y = bld(vr, (unsigned)uu * 4u, kPH * 4);
         pv.z = bld(vr, (unsigned)uu * 4u, 2 * kPH * 4);
         pv.w = bld(w0r, (unsigned)uu * 4u, 0);
     };
-    // The ring entry of step tau for cell (row n, unit / class u), formed by waves 4-7 (no
-    // epilogue cells; idle while waves 0-3 run the fc3 epilogue, hop D and GRU1):
-    //  * P1(tau) as k_persist's ring producers form it (kernels_persist.hip p1_loads / p1_store:
-    //    k_p1_expand's fma chain without its zero tap) from the per-frame tables (a.p1q,
-    //    runtime.hip pack_p1): the phase's 4 taps, 4 frame rows of Q and one of Aq -- no
+    // The per-step operands of cell (row n, unit / class 16 w + j), formed by waves 4-7 (no
+    // epilogue cells; idle while waves 0-3 run the fc3 epilogue, hop D and GRU1) into one-slot
+    // LDS rings -- produced and consumed by the slot itself, so they never leave the CU (round 4
+    // kept them in a 4-slot global ring whose L2 write-backs were 8 GB per C4 launch):
+    //  * noise_make: the Gumbel noise of (tau, row, class) in k_gumbel's fixed-point form
+    //    (philox.h gumbel_q_of) -- no [S][B][n] noise stream; formed for step t + 1 in step t's
+    //    hop-D window (the slot's step-t values were read before that step's stage-D barrier);
+    //  * p1_make: P1(tau) as k_persist's ring producers form it (kernels_persist.hip p1_loads /
+    //    p1_store: k_p1_expand's fma chain without its zero tap) from the per-frame tables
+    //    (a.p1q, runtime.hip pack_p1): the phase's 4 taps, 4 frame rows of Q and one of Aq -- no
     //    [S][B][4H] stream; with WRNN_P1_RING=0 (a.p1q null) copied from that stream instead;
-    //  * the Gumbel noise of (tau, row, class u) in k_gumbel's fixed-point form (philox.h
-    //    gumbel_q_of) -- no [S][B][n] noise stream either.
-    auto ring_make = [&](int n, int u, int tau) {
-        // (a time-sliced row at offset off: its own steps end at S, its noise is drawn at its
-        // absolute step)
+    //    formed for step t + 2 in step t's hop-D window (GRU1 at the end of step t + 1 reads it).
+    // (a time-sliced row at offset off: its own steps end at S, its noise is drawn at its
+    // absolute step)
+    auto noise_make = [&](int n, int j, int tau) {
         const int off = ROT ? reinterpret_cast<const int2*>(lds + WL_VM)[n].y : 0;
-        const int tc = tau < a.S - off ? tau : a.S - off - 1;
-        int uu = u;
+        int uu = 16 * w + j;
         asm volatile("" : "+v"(uu));
         const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
-        const unsigned cell_i = (unsigned)((tau & 3) * 16 * kPH + n * kPH + uu);
-        {
-            // the noise of class u (a padding class beyond n_classes is drawn and never used)
-            const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)(tau + off), (uint32_t)ri.fold, ri.stream,
-                                       a.k0, a.k1);
-            const uint32_t wd = (uu & 3) == 0 ? o.x : (uu & 3) == 1 ? o.y : (uu & 3) == 2 ? o.z : o.w;
-            __builtin_amdgcn_raw_buffer_store_b32(gumbel_q_of(wd), rr, (unsigned)WR_G * 4u + cell_i * 4u, 0, 0);
+        // (a padding class beyond n_classes is drawn and never used)
+        const U4 o = philox4x32_10((uint32_t)(uu >> 2), (uint32_t)(tau + off), (uint32_t)ri.fold, ri.stream,
+                                   a.k0, a.k1);
+        const uint32_t wd = (uu & 3) == 0 ? o.x : (uu & 3) == 1 ? o.y : (uu & 3) == 2 ? o.z : o.w;
+        lds[WL_GR + n * NC + j] = __uint_as_float(gumbel_q_of(wd));
+        if constexpr (C10) {  // and of class 512 + u
+            __builtin_amdgcn_sched_barrier(0);
+            const U4 o2 = philox4x32_10((uint32_t)((uu + kPH) >> 2), (uint32_t)(tau + off), (uint32_t)ri.fold,
+                                        ri.stream, a.k0, a.k1);
+            const uint32_t wd2 = (uu & 3) == 0 ? o2.x : (uu & 3) == 1 ? o2.y : (uu & 3) == 2 ? o2.z : o2.w;
+            lds[WL_GR + n * NC + 16 + j] = __uint_as_float(gumbel_q_of(wd2));
         }
-        __builtin_amdgcn_sched_barrier(0);  // (the noise's temporaries die before the P1 loads)
+    };
+    auto p1_make = [&](int n, int j, int tau) {
+        const int off = ROT ? reinterpret_cast<const int2*>(lds + WL_VM)[n].y : 0;
+        const int tc = tau < a.S - off ? tau : a.S - off - 1;
+        int uu = 16 * w + j;
+        asm volatile("" : "+v"(uu));
+        const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + WL_RI)[n];
         float4 v;
         if (a.p1q == nullptr) {
             // (uniform base + 32-bit lane offset: a per-lane 64-bit address spilled)
@@ -420,16 +436,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             }
             v = make_float4(p_add(m.x, ta.x), p_add(m.y, ta.y), p_add(m.z, ta.z), p_add(m.w, ta.w));
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rr, cell_i * 16u, 0, 0);
+        reinterpret_cast<float4*>(lds + WL_P1R)[n * 16 + j] = v;
     };
     const bool lo = v < 4;  // waves 0-3 hold the epilogue cells
     __syncthreads();  // RowInfo in LDS
-    // ring prologue: steps t0, t0 + 1, t0 + 2 (the loop forms t + 3 at step t). Drained before
-    // the barrier: the first reads come right after it.
+    // ring prologue: the noise of step t0 and P1(t0 + 1) (the loop forms the noise of t + 1 and
+    // P1(t + 2) at step t); the first reads come after the barrier
     if (!lo && tid - 256 < 16 * R) {
         const int i = tid - 256;
-        for (int k = 0; k < 3; ++k) ring_make(i >> 4, 16 * w + (i & 15), a.t0 + k);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        noise_make(i >> 4, i & 15, a.t0);
+        p1_make(i >> 4, i & 15, a.t0 + 1);
     }
     __syncthreads();
     // initial hop E: x1, h1 of step t0 (k_persist_init) as step t0 + 1 (canonicalised: a
@@ -594,9 +610,39 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             }
             pub(WB_Y2, y, seq);
         }
+        if constexpr (C10) {
+            // gh1 = W_hh1 h1 + b_hh1 and gh2 = W_hh2 h2 + b_hh2 now (hop D without C10): PH then
+            // takes the second tile's partials (written after the stage-D barrier, which every
+            // wave reaches after these reads)
+            if (lo && cell) {
+                float gs[6];
+                psums(I3(), WL_PH, 3, gs);
+                psums(I3(), WL_PA, 3, gs + 3);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) gs[j] = p_add(gs[j], lds[WL_BIAS + 16 * j + cul]);
+                g1r = gs[0];
+                g1z = gs[1];
+                g1n = gs[2];
+                g2r = gs[3];
+                g2z = gs[4];
+                g2n = gs[5];
+            }
+        }
         // ================= hop C -> stage D: fc3 y2 (critical) =============================
         fail |= !w_poll(xr, o_cons, so_y2, bvalid, cc, a.ctl, wh(8), (unsigned)t);
-        prefetch_d(t);
+        // C10: the second fc3 tile's A operands of this wave (k-step ks: fb[ks / 4] component
+        // ks % 4, the register tiles' order), L2-resident, in flight over the first tile
+        float4 fb[4];
+        if constexpr (C10) {
+            const rsrc_t fr = mk_rsrc(a.wfc3b + (size_t)(w * 8 + v) * 4 * 64);
+            int ll = l;
+            asm volatile("" : "+v"(ll));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                fb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(fr, (unsigned)ll * 16u,
+                                                                                         (unsigned)q * 1024u, 0));
+        }
+        if constexpr (!C10) prefetch_d();
         WSTAMP(8);
         {
             v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -606,6 +652,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                 acc1 = mfma4(WR(8, ks + 1), bop(cc, ks + 1), acc1);
             }
             *reinterpret_cast<v4f*>(lds + WL_PS + (v * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
+        }
+        if constexpr (C10) {
+            v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+                acc0 = mfma4(f4c(fb[ks >> 2], ks & 3), bop(cc, ks), acc0);
+                acc1 = mfma4(f4c(fb[ks >> 2], (ks + 1) & 3), bop(cc, ks + 1), acc1);
+            }
+            wbar();  // (every wave's gh1 / gh2 reads of PH are done)
+            *reinterpret_cast<v4f*>(lds + WL_PH + (v * 16 + bn) * 16 + wsw(bn, 4 * (l >> 4))) = acc0 + acc1;
+            prefetch_d();  // (after the products: fewer registers live over them)
         }
         if (fail) lds[WL_FAIL] = 1.f;
         wbar();
@@ -625,6 +682,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
                     const CandKey k = cand_key(lg, __float_as_uint(pg), cu);
                     kh = k.hi;
                     kl = k.lo;
+                    if constexpr (C10) {  // class 512 + cu (tile b, partials in PH)
+                        if (kPH + cu < a.n_classes) {
+                            float s2;
+                            psums(I1(), WL_PH, 1, &s2);
+                            const float lg2 = p_add(s2, lds[WL_BIAS + 112 + cul]);
+                            p_dbg_logit<DBG>(a.dbg, t + (ROT ? reinterpret_cast<const int2*>(lds + WL_VM)[cn].y : 0),
+                                             crow, kPH + cu, a.B, a.n_classes, lg2);
+                            int c2 = kPH + cu;
+                            asm volatile("" : "+v"(c2));  // (a hoisted class constant spilled)
+                            const CandKey k2 = cand_key(lg2, __float_as_uint(pg2), c2);
+                            kmax_take(kh, kl, k2.hi, k2.lo);
+                        }
+                    }
                 }
                 row16_kmax(kh, kl);
                 if (cell && cul == 0)
@@ -635,8 +705,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             // from the off-path partials, while the candidates travel: every wave wrote them
             // before the stage C barrier. PH is rewritten in the next hop-A wait, after the next
             // stage-A barrier; PA in the next stage A behind a barrier of its own (see there):
-            // this wave reaches both only after these reads have completed.
-            if (cell) {
+            // this wave reaches both only after these reads have completed. (C10: read in the
+            // hop-C wait, see there)
+            if (!C10 && cell) {
                 float gs[6];
                 psums(I3(), WL_PH, 3, gs);
                 psums(I3(), WL_PA, 3, gs + 3);
@@ -706,12 +777,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
             pub(WB_X1, x1, seq + 1u);
             pub(WB_H1, h1r, seq + 1u);
         } else {
-            // waves 4-7: ring entry of step t + 3 for cell i = tid - 256 (written three steps
-            // ahead: its stores are drained by this wave's next poll, before the next stage-A
-            // barrier, and waves 0-3 read it two steps later; slot (t + 3) & 3 last held step
-            // t - 1, whose reads ended in step t - 1)
+            // waves 4-7: the noise of step t + 1 and P1(t + 2) for cell i = tid - 256 into the
+            // one-slot LDS rings (waves 0-3 read the slots' step-t / P1(t + 1) values in
+            // prefetch_d, before this step's stage-D barrier, and the new ones after the next
+            // step's stage-A barrier)
             const int i = tid - 256;
-            if (i < 16 * R) ring_make(i >> 4, 16 * w + (i & 15), t + 3);
+            if (i < 16 * R) {
+                noise_make(i >> 4, i & 15, t + 1);
+                p1_make(i >> 4, i & 15, t + 2);
+            }
         }
         if (w == 0 && tid == 0) {
             if (g == 0) p_progress(a.progress, a.prog_base, t);
@@ -754,7 +828,7 @@ hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s) {
     k_wide_xbuf_reset<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<uint4*>(xbuf));
     return hipGetLastError();
 }
-size_t persist_wide_ring_floats() { return (size_t)kPG * WR_GROUP; }
+size_t persist_wide_ring_floats() { return 64; }  // (no global ring since round 5: LDS rings)
 
 // Exhaustive host-side check of the exchange layout for a group of R rows (wide_layout.h): the
 // producer packets of one hop slot (32 slots x R rows x 4 unit quads) and the consumer packets
@@ -807,28 +881,36 @@ int wide_layout_check(int R) {
 size_t persist_wide_wreg_floats() { return (size_t)kPM * 8 * 4 * kWTiles * 64 * 4; }
 size_t persist_wide_wlds_floats() { return (size_t)kPM * WL_HH2_SZ; }
 
-int persist_wide_scratch() {
+int persist_wide_scratch(bool c10) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<false, false>) != hipSuccess) return -1;
+    const void* f = c10 ? (const void*)k_persist_wide<false, true, false> : (const void*)k_persist_wide<false, false, false>;
+    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
-int persist_wide_rot_scratch() {
+int persist_wide_rot_scratch(bool c10) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide<true, false>) != hipSuccess) return -1;
+    const void* f = c10 ? (const void*)k_persist_wide<true, true, false> : (const void*)k_persist_wide<true, false, false>;
+    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s) {
-    if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > kPM * 16 ||
-        a.mode != 0 || a.wwide == nullptr || a.wring == nullptr)
+    if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.n_classes > 2 * kPM * 16 ||
+        a.mode != 0 || a.wwide == nullptr || (a.n_classes > kPM * 16 && a.wfc3b == nullptr))
         return hipErrorInvalidValue;
-    if (a.vmap) {
-        if (a.p1q == nullptr) return hipErrorInvalidValue;  // time-sliced rows: P1 formed in-kernel
-        if (a.dbg.out) return persist_launch<k_persist_wide<true, true>>(persist_wide_lds_bytes(), a, s);
-        return persist_launch<k_persist_wide<true, false>>(persist_wide_lds_bytes(), a, s);
+    const size_t lb = persist_wide_lds_bytes();
+    const bool dbg = a.dbg.out != nullptr;
+    if (a.vmap && a.p1q == nullptr) return hipErrorInvalidValue;  // time-sliced rows: P1 formed in-kernel
+    if (a.n_classes > kPM * 16) {
+        if (a.vmap) return dbg ? persist_launch<k_persist_wide<true, true, true>>(lb, a, s)
+                               : persist_launch<k_persist_wide<true, true, false>>(lb, a, s);
+        return dbg ? persist_launch<k_persist_wide<false, true, true>>(lb, a, s)
+                   : persist_launch<k_persist_wide<false, true, false>>(lb, a, s);
     }
-    if (a.dbg.out) return persist_launch<k_persist_wide<false, true>>(persist_wide_lds_bytes(), a, s);
-    return persist_launch<k_persist_wide<false, false>>(persist_wide_lds_bytes(), a, s);
+    if (a.vmap) return dbg ? persist_launch<k_persist_wide<true, false, true>>(lb, a, s)
+                           : persist_launch<k_persist_wide<true, false, false>>(lb, a, s);
+    return dbg ? persist_launch<k_persist_wide<false, false, true>>(lb, a, s)
+               : persist_launch<k_persist_wide<false, false, false>>(lb, a, s);
 }
 
 }  // namespace wrnn

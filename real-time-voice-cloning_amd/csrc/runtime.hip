@@ -203,6 +203,7 @@ struct wrnn_handle {
         const float *p1taps = nullptr, *zero_np = nullptr;
         int p1split = -1;  // phase from which the 4 in-kernel taps start at frame f - 1
         const float *wwide = nullptr, *wwide_lds = nullptr;  // wide-row launches (MFMA images)
+        const float* wfc3b = nullptr;  // ... > 512 classes: the second fc3 tile (L2-streamed)
         const float* wwide_rr = nullptr;  // runtimeracer wide-row launches (kernels_persist_wide_rr.hip)
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
@@ -636,13 +637,14 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
 // Wide-row launch weight images (kernels_persist_wide.hip): MFMA A operands. Slot w, wave v,
 // lane l, tile T, k-step ks: W_T[row 16 w + (l & 15)][unit 64 v + 16 (l >> 4) + ks]; registers
 // [w][v][40 float4 (4 T + ks / 4)][64 l] for T = W_ih2[:, :512] r, z, n | W_hh1 r, z, n | fc1 |
-// fc2 | fc3 (x parts only), LDS [w][3 T][v][4 q][64 l][4] for W_hh2 r, z, n.
+// fc2 | fc3 (x parts only), LDS [w][3 T][v][4 q][64 l][4] for W_hh2 r, z, n; above 512 classes
+// the second fc3 tile (rows 512 + 16 w + i) as [w][v][4 q][64 l] float4, read per step.
 int pack_persist_wide(wrnn_handle* h) {
     auto& T = h->host;
     auto& P = h->pw;
-    P.wwide = P.wwide_lds = nullptr;
+    P.wwide = P.wwide_lds = P.wfc3b = nullptr;
     const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
-    if (h->cfg.mode != WRNN_MODE_RAW || n > kPM * 16 || H != kPH || F != kPH) return WRNN_OK;
+    if (h->cfg.mode != WRNN_MODE_RAW || n > 2 * kPM * 16 || H != kPH || F != kPH) return WRNN_OK;
     const auto& Wih2 = T["rnn2.weight_ih_l0"];  // (3H, H + A)
     const auto& Whh1 = T["rnn1.weight_hh_l0"];  // (3H, H)
     const auto& Whh2 = T["rnn2.weight_hh_l0"];  // (3H, H)
@@ -678,6 +680,19 @@ int pack_persist_wide(wrnn_handle* h) {
                                 elem(w, 9 + t, l & 15, 64 * v + 16 * (l >> 4) + 4 * q + c);
             }
     int rc = WRNN_OK;
+    if (n > kPM * 16) {
+        std::vector<float> wb((size_t)kPM * 8 * 4 * 64 * 4);
+        for (int w = 0; w < kPM; ++w)
+            for (int v = 0; v < 8; ++v)
+                for (int q = 0; q < 4; ++q)
+                    for (int l = 0; l < 64; ++l)
+                        for (int c = 0; c < 4; ++c) {
+                            const int u = kPM * 16 + 16 * w + (l & 15), k = 64 * v + 16 * (l >> 4) + 4 * q + c;
+                            wb[((((size_t)w * 8 + v) * 4 + q) * 64 + l) * 4 + c] = u < n ? Wf3[(size_t)u * F + k] : 0.f;
+                        }
+        P.wfc3b = upload(h, wb, &rc);
+        CHECK(rc);
+    }
     P.wwide = upload(h, wr, &rc);
     CHECK(rc);
     P.wwide_lds = upload(h, wl, &rc);
@@ -1885,8 +1900,9 @@ bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan&
 }
 
 // Time-sliced wide launches. The wide kernel's step costs nearly the same for
-// any row count up to 16 per group (MFMA tiles of 16 columns), so R = 8 R_g rows with
-// 16 < R_g <= 32 run best as launches of 16 rows per group over rotating row sets: with
+// any row count up to 16 per group (MFMA tiles of 16 columns), so R = 8 R_g rows with R_g > 16
+// (not a multiple of 16; at most 64 launches) run best as launches of 16 rows per group over
+// rotating row sets: with
 // d = R_g - 16 rows of each group idle per launch (a circular shift by gcd(R_g, d) rows per
 // launch), K = R_g / gcd launches make every row active in A = 16 K / R_g of them; each runs
 // n = S / A steps (integer part), and ceil(R_g / 16) short launches give every row the remaining
@@ -1896,8 +1912,9 @@ bool plan_wide_slices(int R, int S, std::vector<wrnn_handle::WLaunch>& out) {
     out.clear();
     if (R % kPG) return false;
     const int Rg = R / kPG;
-    if (Rg <= kPWideRows || Rg > 2 * kPWideRows) return false;
+    if (Rg <= kPWideRows || Rg % kPWideRows == 0) return false;  // (a multiple of 16: full launches)
     const int d = Rg - kPWideRows, gg = gcd_i(Rg, d), K = Rg / gg, A = kPWideRows * K / Rg;
+    if (K > 64) return false;
     const int n = S / A, rem = S - A * n;
     if (n < 64) return false;
     std::vector<int> off(R, 0);
@@ -2131,6 +2148,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const int nb = (int)h->p_plan.size();
     a.wwide = (const float4*)W.wwide;
     a.wwide_lds = (const float4*)W.wwide_lds;
+    a.wfc3b = (const float4*)W.wfc3b;
     if (any_wide) {  // the wide kernels form P1 and the noise in-kernel into this ring
         CHECK(P.wring.alloc((rr ? persist_wide_rr_ring_floats() : persist_wide_ring_floats()) * sizeof(float)));
         a.wring = P.wring.f();
@@ -2443,6 +2461,7 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
 // per-step cost of a runtimeracer wide-row launch at 1 row per group, for the launch plan
 // (MI355X, bench HIP events)
 static const double kWideRRUs = 12.0;  // 12.39 us at 15-16 rows (profiles/r04/wide_rr/)
+static const double kWide10Us = 0.8;   // fatchord wide, 1024 classes: the second fc3 tile (estimate)
 
 int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
@@ -2531,13 +2550,16 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
             if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
             // (a variant with register spills is not used unless WRNN_WIDE_ALLOW_SCRATCH=1: A/B)
-            const bool scratch_ok = persist_wide_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
+            const bool c10 = h->n_classes > kPM * 16;
+            const bool scratch_ok = persist_wide_scratch(c10) == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
             if (wmode && h->pw.wwide && scratch_ok) {
                 if (wmode == 1) opts.clear();
                 // measured per step: round 2 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows
                 // per group (the MFMA tiles cost the same for any row count; the exchanges and
-                // epilogues grow a little with the rows); round 3 11.38 at 16 -- fit 10.5 + 0.055 r
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, 10.5 + 0.055 * r});
+                // epilogues grow a little with the rows); round 3 11.38 at 16 -- fit 10.5 + 0.055 r;
+                // 1024 classes (the second fc3 tile): + kWide10Us
+                for (int r = 1; r <= kPWideRows; ++r)
+                    opts.push_back({r, true, 10.5 + 0.055 * r + (c10 ? kWide10Us : 0.0)});
             }
         } else {
             // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us
@@ -2597,10 +2619,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         const char* e1 = std::getenv("WRNN_PERSIST_SLICE");
         const char* e2 = std::getenv("WRNN_PERSIST_WIDE");
         std::vector<wrnn_handle::WLaunch> sl;
-        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && persist_wide_rot_scratch() == 0 &&
+        const bool c10 = h->n_classes > kPM * 16;
+        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && persist_wide_rot_scratch(c10) == 0 &&
             plan_wide_slices(B, S, sl)) {
             double cost = 60.0 * (sl.size() - 1);  // (an extra launch: weights, ring prologue)
-            for (const auto& L : sl) cost += L.steps * (10.5 + 0.055 * L.nr);
+            for (const auto& L : sl) cost += L.steps * (10.5 + 0.055 * L.nr + (c10 ? kWide10Us : 0.0));
             if (cost < 0.98 * plan_us * S) {
                 lplan.clear();
                 for (int j = 0; j < (int)sl.size(); ++j) lplan.push_back({0, sl[j].nr, true, j});

@@ -239,7 +239,8 @@ struct PersistArgs {
     // wide-row launches (kernels_persist_wide.hip): MFMA A-operand weight images
     const float4* wwide;    // [kPM][8 waves][40 float4][64 lanes]
     const float4* wwide_lds;// [kPM][2 tiles][8][4][64] (W_hh2 z, n)
-    float* wring;           // wide launches: per-group ring of P1 and noise (persist_wide_ring_floats)
+    const float4* wfc3b;    // > 512 classes: fc3 rows 512 + 16 w + i, [kPM][8 waves][4][64 lanes]
+    float* wring;           // runtimeracer wide launches: per-group ring of P1 and noise
     DbgLogits dbg;
     // rotated launch (k_persist; null otherwise): virtual row v = g + 8 r ->
     // (physical row, step offset), rows per group (nr or nr - 1), steps per group; `rows` is then
@@ -251,7 +252,7 @@ struct PersistArgs {
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 // Wide-row fatchord launch: up to kPWideRows rows per XCD group (8 kPWideRows per launch),
-// fp32 MFMA products, RAW categorical with <= 512 classes.
+// fp32 MFMA products, RAW categorical with <= 1024 classes (> 512: PersistArgs::wfc3b).
 constexpr int kPWideRows = 16;
 hipError_t launch_persist_wide(const PersistArgs& a, hipStream_t s);
 size_t persist_wide_lds_bytes();
@@ -260,8 +261,8 @@ hipError_t persist_wide_reset_xbuf(float* xbuf, hipStream_t s);
 size_t persist_wide_ring_floats();
 size_t persist_wide_wreg_floats();
 size_t persist_wide_wlds_floats();
-int persist_wide_scratch();
-int persist_wide_rot_scratch();  // the time-sliced instance (PersistArgs::vmap)
+int persist_wide_scratch(bool c10 = false);      // (c10: the 1024-class instances)
+int persist_wide_rot_scratch(bool c10 = false);  // the time-sliced instance (PersistArgs::vmap)
 int wide_layout_check(int rows_per_group);  // host: violations of the exchange layout (wide_layout.h)
 hipError_t launch_persist_init(const PersistArgs& a, hipStream_t s);
 constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL noise

@@ -26,9 +26,11 @@ pytestmark = pytest.mark.gpu
 LOGIT_ABS_TOL = 1e-5
 
 CASES = [(k, e) for k in golden_meta() for e in ('persist', 'chain')]
-# the wide MFMA launch (kernels_persist_wide.hip) on the fatchord RAW <= 512-class fixtures
+# the wide MFMA launches (kernels_persist_wide.hip, fatchord RAW up to 1024 classes;
+# kernels_persist_wide_rr.hip, runtimeracer)
 WIDE = ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny', 'fatchord_raw9_config1',
-        'fatchord_raw9_c2_peaked', 'runtimeracer_raw9_tiny', 'runtimeracer_raw10_defaults']
+        'fatchord_raw9_c2_peaked', 'fatchord_raw10_defaults', 'fatchord_raw10_unbatched_tiny',
+        'fatchord_raw10_peaked_defaults', 'runtimeracer_raw9_tiny', 'runtimeracer_raw10_defaults']
 
 
 def _run(name, engine, wide=False, monkeypatch=None):

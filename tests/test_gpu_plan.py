@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run(model_type, mode, bits, n_utts, frames=1000):
+def _run(model_type, mode, bits, n_utts, frames=1000, target=11000, overlap=550):
     import torch
     from wavernn_amd.base import hparams_for
     from wavernn_amd.hparams import sp
@@ -23,7 +23,7 @@ def _run(model_type, mode, bits, n_utts, frames=1000):
     m.load_state_dict(synth_state_dict(hp, model_type, seed=0))
     mels = [torch.from_numpy((synth_mel(frames, u) / sp.max_abs_value).astype(np.float32)).cuda()
             for u in range(n_utts)]
-    m.generate_batch_device(mels, True, 11000, 550)
+    m.generate_batch_device(mels, True, target, overlap)
     assert m.last_engine() == 'persist'
     return m.plan_info()
 
@@ -55,3 +55,12 @@ def test_c4_shape_is_time_sliced_over_wide_launches(monkeypatch):
     plan = _run('fatchord-wavernn', 'RAW', 9, 8)
     assert sorted((nr, wide) for _, nr, wide in plan) == [(2, False), (16, True)]
     assert sum(8 * nr for _, nr, _ in plan) == 144
+
+
+def test_fatchord_10bit_default_batch_is_time_sliced_over_wide_launches():
+    """The fork's fatchord default (10 bits, target 3,000 / overlap 1,500: 45 rows per 1000-frame
+    utterance) at 8 utterances: 360 rows, 45 per group -- 45 time-sliced wide launches of 16 rows
+    per group x 375 steps on the 1024-class instances (VERDICT r4 missing #3), no
+    register-resident launch."""
+    plan = _run('fatchord-wavernn', 'RAW', 10, 8, target=3000, overlap=1500)
+    assert plan == [(0, 16, True)] * 45, plan

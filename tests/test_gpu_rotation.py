@@ -14,12 +14,12 @@ pytestmark = pytest.mark.gpu
 TARGET, OVERLAP = 4000, 400  # 4,800 steps (shorter calls do not pay for the extra launches)
 
 
-def _model(mode='RAW'):
+def _model(mode='RAW', bits=9):
     from wavernn_amd.base import hparams_for
     from wavernn_amd.hparams import sp
     from wavernn_amd.model import WaveRNN
     from wavernn_amd.synth import synth_state_dict
-    hp = hparams_for('fatchord-wavernn').copy(bits=9, mode=mode)
+    hp = hparams_for('fatchord-wavernn').copy(bits=bits, mode=mode)
     m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels, hp.compute_dims,
                 hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate, mode=mode,
                 model_type='fatchord-wavernn', device=0)
@@ -106,16 +106,18 @@ def test_rotated_call_reports_progress_at_the_reference_cadence(monkeypatch):
     assert np.array_equal(a, b_)
 
 
-def test_time_sliced_wide_equals_wide_plus_tail(monkeypatch):
+@pytest.mark.parametrize('bits', [9, 10])
+def test_time_sliced_wide_equals_wide_plus_tail(bits, monkeypatch):
     """8 utterances x 18 rows (the C4 shape at 4,800 steps): the time-sliced wide launches (every
     row through 16-row-per-group wide launches at its own offsets, state across launches) give
     the labels of the wide 128-row launch + register-resident 16-row launch plan
     (WRNN_PERSIST_SLICE=0) bit for bit, and so do the wide rows' logits recorded around the slice
-    boundaries (600 steps per launch at 4,800 steps: 8 of 9 launches per row)."""
+    boundaries (600 steps per launch at 4,800 steps: 8 of 9 launches per row). 10 bits: the
+    1024-class instances."""
     import torch
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    m, hp = _model()
+    m, hp = _model(bits=bits)
     T = _frames_for(m, 18)
     devs = [torch.from_numpy((synth_mel(T, 40 + u) / sp.max_abs_value).astype(np.float32)).cuda() for u in range(8)]
     steps = [0, 599, 600, 601, 1199, 1200, 2400, 4799]

@@ -31,8 +31,10 @@ def _stage_names(m):
 
 
 @pytest.mark.parametrize('name', ['fatchord_raw9_tiny', 'fatchord_raw9_sharp_tiny',
-                                  'fatchord_raw9_config1', 'fatchord_raw9_c2_peaked'])
+                                  'fatchord_raw9_config1', 'fatchord_raw9_c2_peaked',
+                                  'fatchord_raw10_defaults', 'fatchord_raw10_unbatched_tiny'])
 def test_wide_golden_bit_exact(name, wide_only):
+    """(10-bit: the 1024-class instances, a second fc3 tile per slot streamed from L2)"""
     meta, gold = golden_case(name)
     from test_gpu_parity import make_model
     from wavernn_amd.hparams import sp

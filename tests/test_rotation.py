@@ -83,13 +83,13 @@ def slice_plan(R, S=12100):
     return K, np.array(rs[:2 * K]).reshape(K, 2), np.array(vm[:K * 128 * 2]).reshape(K, 16, 8, 2)
 
 
-@pytest.mark.parametrize('R', [136, 144, 160, 192, 256])
+@pytest.mark.parametrize('R', [136, 144, 160, 192, 264, 360])
 def test_wide_time_slices_plan_invariants(R):
     """Time-sliced wide launches: at most 16 rows per group and launch, every
     row at most once per launch and in its own group (rows g + 8 i), offsets advanced by the
     launch's steps, every row at exactly S. C4 (144 rows): 9 launches of 1,512 steps at 16 rows
     per group, then 2 of the remaining 4 steps (16 and 2 rows per group)."""
-    S = 12100
+    S = 12100 if R < 300 else 6000
     K, rs, vm = slice_plan(R, S)
     assert K > 1
     off = np.zeros(R, int)
@@ -112,6 +112,6 @@ def test_wide_time_slices_plan_invariants(R):
         assert K == 11 and rs[:9].tolist() == [[16, 1512]] * 9 and rs[9:].tolist() == [[16, 4], [2, 4]]
 
 
-@pytest.mark.parametrize('R', [128, 120, 143, 264, 18])
-def test_wide_time_slices_only_between_16_and_32_rows_per_group(R):
+@pytest.mark.parametrize('R', [128, 120, 143, 256, 384, 18])
+def test_wide_time_slices_only_above_16_rows_per_group_and_off_multiples_of_16(R):
     assert slice_plan(R)[0] == 0
