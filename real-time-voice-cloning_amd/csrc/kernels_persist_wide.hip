@@ -189,6 +189,9 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 //      L2-resident) are loaded every step in the hop-C wait -- the registers hold the other nine
 //      tiles; its partials go to PH after one more barrier (the gh1 / gh2 partial sums are read
 //      in the hop-C wait instead of hop D, so PH is free by then)
+#ifndef WRNN_FC3B_POL
+#define WRNN_FC3B_POL 0  // cache policy of the second fc3 tile's loads (A/B: 2 = non-temporal)
+#endif
 template <bool ROT, bool C10, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
@@ -640,7 +643,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 fb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(fr, (unsigned)ll * 16u,
-                                                                                         (unsigned)q * 1024u, 0));
+                                                                                         (unsigned)q * 1024u, WRNN_FC3B_POL));
         }
         if constexpr (!C10) prefetch_d();
         WSTAMP(8);

@@ -12,6 +12,7 @@ run() {  # name, kernel regex, counters, bench args
 }
 run c4_write k_persist_wide "WRITE_SIZE" "$C4"
 run c4_wb k_persist_wide "TCC_NORMAL_WRITEBACK_sum TCC_ALL_TC_OP_WB_WRITEBACK_sum TCC_NORMAL_EVICT_sum TCC_EA0_WRREQ_sum" "$C4"
+run b10_write k_persist_wide "WRITE_SIZE" "--utts-per-gpu 8 --bits 10 --target 3000 --overlap 1500 --steps 2 --warmup 1 --cpu-seconds 0 --no-timing"
 run c2_wb "k_persist[^_]" "TCC_NORMAL_WRITEBACK_sum TCC_ALL_TC_OP_WB_WRITEBACK_sum TCC_NORMAL_EVICT_sum TCC_EA0_WRREQ_sum" "$C2"
 python3 - $OUT <<'PY'
 import csv, glob, sys, collections
