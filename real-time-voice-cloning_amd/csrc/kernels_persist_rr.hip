@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         for (int i = tid; i < 32 * RK4; i += kPT) d5[i] = s5[i];
     }
     // ---- chunk state ----------------------------------------------------------------------
-    const size_t SW = 11 * RH;  // state floats per row
+    const size_t SW = (size_t)kRRState * RH;  // state floats per row
     float h1[NRH];
 #pragma unroll
     for (int i = 0; i < NRH; ++i) {
@@ -748,13 +748,13 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     }}
 
 // Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0); h2 = h3 = h4 = 0,
-// gh2 = b_hh2, gh3 = b_hh3.
+// gh2 = b_hh2, gh3 = b_hh3, gh4 = b_hh4.
 __global__ __launch_bounds__(kRH) void k_persist_rr_init(PersistRRArgs a) {
     const int row = blockIdx.x, j = threadIdx.x, H = kRH;
     const float* P1 = a.P1 + ((size_t)row * H + j) * 4;  // step 0: (r, z, n, cI) of unit j
     const float hn = p_gru(P1[0], P1[1], P1[2], a.b_hh1[j], a.b_hh1[H + j],
                            a.b_hh1[2 * H + j], 0.f);
-    float* st = a.st + (size_t)row * 11 * H;
+    float* st = a.st + (size_t)row * kRRState * H;
     st[j] = p_add(P1[3], hn);
     st[H + j] = hn;
     st[2 * H + j] = 0.f;
@@ -764,6 +764,7 @@ __global__ __launch_bounds__(kRH) void k_persist_rr_init(PersistRRArgs a) {
     for (int k = 0; k < 3; ++k) {
         st[5 * H + k * H + j] = a.b_hh2[k * H + j];
         st[8 * H + k * H + j] = a.b_hh3[k * H + j];
+        st[11 * H + k * H + j] = a.b_hh4[k * H + j];
     }
 }
 

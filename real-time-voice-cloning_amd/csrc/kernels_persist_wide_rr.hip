@@ -77,7 +77,8 @@ constexpr int RG_SLOT = RG_P + 4 * kRowsW * 64;
 constexpr int QL_RI = 0;         // RowInfo of the group's rows (6 words each)
 constexpr int QL_FAIL = 112;
 constexpr int QL_REG = 116;      // group, slot, registration result (ints)
-constexpr int QL_CB = 128;       // slot constants (biases), see the halves
+constexpr int QL_CB = 128;       // slot constants (biases), see the halves (<= 224 floats)
+constexpr int QL_VM = 448;       // (physical row, step offset) of each row slot (int2, ROT)
 constexpr int QL_P = 512;        // partial tiles [8 v][nt][16 n][16 m], one buffer per product
 constexpr int T3 = 8 * 3 * 256, T1 = 8 * 256;
 // half A
@@ -89,6 +90,7 @@ constexpr int PB_H1 = QL_P, PB_G3 = PB_H1 + T3, PB_H3 = PB_G3 + T3, PB_F1 = PB_H
 constexpr int QL_TOTAL = PA_END > PB_END ? PA_END : PB_END;
 static_assert(QL_TOTAL * 4 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 static_assert(sizeof(RowInfo) == 24 && kRowsW * 6 <= QL_FAIL, "RowInfo array overflows");
+static_assert(QL_CB + 224 <= QL_VM && QL_VM + 2 * kRowsW <= QL_P, "small LDS arrays overflow");
 
 constexpr int kWq = 30;  // float4 weight registers per lane: 15 tiles x 8 k-steps
 
@@ -145,7 +147,10 @@ __device__ __forceinline__ bool q_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 }  // namespace
 
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-template <bool DBG>
+// ROT: a time-sliced launch (PersistRRArgs::vmap): row slot r of group g is the
+//      virtual row g + 8 r -> (physical row, step offset); the launch runs steps [0, t1) of its
+//      rows (their steps off .. off + t1 - 1) from the chunk state and saves it at the end
+template <bool ROT, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     int* sreg = reinterpret_cast<int*>(lds + QL_REG);
@@ -170,7 +175,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
     const int cn = tid >> 4, cul = tid & 15;  // epilogue cell (row cn, unit 16 s + cul), waves 0-3
     const bool cell = tid < 16 * R;
     const int cu = 16 * s + cul;
-    const int crow = g0 + kPG * (cell ? cn : 0);
+    const int crow = ROT ? a.vmap[g0 + kPG * (cell ? cn : 0)].x : g0 + kPG * (cell ? cn : 0);
+    // a row slot's step offset (time-sliced launches; 0 otherwise)
+    auto roff = [&](int n) { return ROT ? reinterpret_cast<const int2*>(lds + QL_VM)[n].y : 0; };
     const rsrc_t xr = mk_rsrc(a.xbuf + (size_t)g * QX_GROUP);
     const rsrc_t rgr = mk_rsrc(a.wring + ((size_t)g * kHalf + s) * RG_SLOT);  // slot s's ring
     const unsigned o_cons = q_cons(v, l);
@@ -192,7 +199,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         for (int q = 0; q < kWq; ++q) wq[q] = src[(size_t)q * 64];
     }
 #define QW(T, ks) f4c(wq[2 * (T) + (ks) / 4], (ks) % 4)
-    if (tid < R) reinterpret_cast<RowInfo*>(lds + QL_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid < R) {
+        reinterpret_cast<RowInfo*>(lds + QL_RI)[tid] = a.rows[g0 + kPG * tid];
+        if (ROT) reinterpret_cast<int2*>(lds + QL_VM)[tid] = a.vmap[g0 + kPG * tid];
+    }
     if (tid == 0) lds[QL_FAIL] = 0.f;
 
     // publish the cell's value of step seq: slot seq & 1, the sentinel into slot (seq + 1) & 1
@@ -266,7 +276,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         float g2r = 0.f, g2z = 0.f, g2n = 0.f, g4r = 0.f, g4z = 0.f, g4n = 0.f;
         const float* cb = lds + QL_CB;
         __syncthreads();
-        if (cell) {  // h2 = h4 = 0 at step 0: gh = W_hh 0 + b_hh
+        if (cell && !ROT) {  // h2 = h4 = 0 at step 0: gh = W_hh 0 + b_hh
             g2r = cb[48 + cul];
             g2z = cb[64 + cul];
             g2n = cb[80 + cul];
@@ -274,16 +284,28 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             g4z = cb[160 + cul];
             g4n = cb[176 + cul];
         }
+        if (cell && ROT) {  // the row's chunk state (k_persist_rr_init or an earlier slice)
+            const float* st = a.st + (size_t)crow * kRRState * RH;
+            h2r = st[2 * RH + cu];
+            h4r = st[4 * RH + cu];
+            g2r = st[5 * RH + cu];
+            g2z = st[6 * RH + cu];
+            g2n = st[7 * RH + cu];
+            g4r = st[11 * RH + cu];
+            g4z = st[12 * RH + cu];
+            g4n = st[13 * RH + cu];
+        }
         // the partner B slot's ring entry of step tau: thread tid < 256 forms P1 of cell
         // (row tid / 16, unit 16 s + tid % 16); thread 256 + i the Gumbel noise of classes
         // cpw s + 4 (i % 16) .. + 3 of row i / 16 (one Philox call, four words)
         auto ring_make = [&](int tau) {
-            const int tc = tau < a.S ? tau : a.S - 1;
             int tx = tid;
             asm volatile("" : "+v"(tx));
             if (tx < 256) {
                 const int n = tx >> 4, uu = 16 * s + (tx & 15);
                 if (n >= R) return;
+                // (a time-sliced row: its own steps end at S)
+                const int tc = tau < a.S - roff(n) ? tau : a.S - roff(n) - 1;
                 const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + QL_RI)[n];
                 float4 vv;
                 if (a.p1q == nullptr) {
@@ -326,7 +348,9 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                 if (n >= R || 4 * jq >= a.cpw) return;
                 const RowInfo& ri = reinterpret_cast<const RowInfo*>(lds + QL_RI)[n];
                 const int c0 = a.cpw * s + 4 * jq;  // classes c0 .. c0 + 3 (cpw % 4 == 0)
-                const U4 o = philox4x32_10((uint32_t)(c0 >> 2), (uint32_t)tau, (uint32_t)ri.fold, ri.stream, a.k0, a.k1);
+                // (drawn at the row's absolute step)
+                const U4 o = philox4x32_10((uint32_t)(c0 >> 2), (uint32_t)(tau + roff(n)), (uint32_t)ri.fold,
+                                           ri.stream, a.k0, a.k1);
                 const u4v gv = {gumbel_q_of(o.x), gumbel_q_of(o.y), gumbel_q_of(o.z), gumbel_q_of(o.w)};
                 __builtin_amdgcn_raw_buffer_store_b128(
                     gv, rgr, (unsigned)(RG_P + ((tau & 3) * kRowsW + n) * 64 + 4 * jq) * 4u, 0, 0);
@@ -459,6 +483,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             RS(13);
         }
         if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
+        if (ROT && cell && lds[QL_FAIL] == 0.f) {  // the rows' state for their next slice
+            int nn = cn;
+            asm volatile("" : "+v"(nn));
+            float* st = a.st + (size_t)reinterpret_cast<const int2*>(lds + QL_VM)[nn].x * kRRState * RH;
+            st[2 * RH + cu] = h2r;
+            st[4 * RH + cu] = h4r;
+            st[5 * RH + cu] = g2r;
+            st[6 * RH + cu] = g2z;
+            st[7 * RH + cu] = g2n;
+            st[11 * RH + cu] = g4r;
+            st[12 * RH + cu] = g4z;
+            st[13 * RH + cu] = g4n;
+        }
     } else {
         // =============================== half B ===================================
         // slot constants: b_hh1, b_hh3 [3][16], b_f5 [cpw] of the slot's classes
@@ -473,12 +510,19 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
         float h1r = 0.f, h3r = 0.f, x1c = 0.f;
         float g1r = 0.f, g1z = 0.f, g1n = 0.f, g3r = 0.f, g3z = 0.f, g3n = 0.f;
         if (cell) {  // x1, h1 of step t0 (k_persist_rr_init), h3 = 0: gh3 = b_hh3
-            const float* st = a.st + (size_t)crow * 11 * RH;
+            const float* st = a.st + (size_t)crow * kRRState * RH;
             x1c = st[cu];
             h1r = st[RH + cu];
-            g3r = a.b_hh3[cu];
-            g3z = a.b_hh3[RH + cu];
-            g3n = a.b_hh3[2 * RH + cu];
+            if (ROT) {  // (a time-sliced row: its chunk state)
+                h3r = st[3 * RH + cu];
+                g3r = st[8 * RH + cu];
+                g3z = st[9 * RH + cu];
+                g3n = st[10 * RH + cu];
+            } else {
+                g3r = a.b_hh3[cu];
+                g3z = a.b_hh3[RH + cu];
+                g3n = a.b_hh3[2 * RH + cu];
+            }
         }
         const float* cb = lds + QL_CB;
         const rsrc_t fcr = mk_rsrc(a.fcond);
@@ -626,7 +670,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                             const int c = a.cpw * s + 16 * j + cul;
                             if (c < a.n_classes) {
                                 const float lg = p_add(ps[j], cb[96 + 16 * j + cul]);
-                                p_dbg_logit<DBG>(a.dbg, t, crow, c, a.B, a.n_classes, lg);
+                                p_dbg_logit<DBG>(a.dbg, t + roff(cn), crow, c, a.B, a.n_classes, lg);
                                 const CandKey k = cand_key(lg, __float_as_uint(pn[j]), c);
                                 kmax_take(kh, kl, k.hi, k.lo);
                             }
@@ -671,7 +715,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                     if (s == 0 && cell && cul == 0) {
                         int nn = cn;
                         asm volatile("" : "+v"(nn));
-                        const unsigned ro = (unsigned)((g0 + kPG * nn) * a.ld);
+                        unsigned ro = (unsigned)((g0 + kPG * nn) * a.ld);
+                        if (ROT) {
+                            const int2 vm = reinterpret_cast<const int2*>(lds + QL_VM)[nn];
+                            ro = (unsigned)(vm.x * a.ld + vm.y);
+                        }
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels), ro * 2u,
                                                               (unsigned)t * 2u, 0);
                         bst(x, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -685,6 +733,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                 if (cell) {
                     h1r = p_gru(fmaf(vr, x, pp.x), fmaf(vz, x, pp.y), fmaf(vn, x, pp.z), g1r, g1z, g1n, h1r);
                     x1 = p_add(fmaf(w0c, x, pp.w), h1r);
+                    if (ROT) x1c = x1;
                 }
                 pub(QX1, x1, seq + 1u);
                 pub(QH1, h1r, seq + 1u);
@@ -694,6 +743,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
                 if (g == 0) p_progress(a.progress, a.prog_base, t);
                 if (p_abort(a.ctl, a.progress, t)) lds[QL_FAIL] = 1.f;  // seen at the half's next check
             }
+        }
+        if (ROT && cell && lds[QL_FAIL] == 0.f) {  // x1, h1 of step t1 (GRU1 of the last step), h3, gh3
+            int nn = cn;
+            asm volatile("" : "+v"(nn));
+            float* st = a.st + (size_t)reinterpret_cast<const int2*>(lds + QL_VM)[nn].x * kRRState * RH;
+            st[cu] = x1c;
+            st[RH + cu] = h1r;
+            st[3 * RH + cu] = h3r;
+            st[8 * RH + cu] = g3r;
+            st[9 * RH + cu] = g3z;
+            st[10 * RH + cu] = g3n;
         }
     }
 #undef QW
@@ -719,18 +779,27 @@ hipError_t persist_wide_rr_reset_xbuf(float* xbuf, hipStream_t s) {
 }
 int persist_wide_rr_scratch() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide_rr<false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide_rr<false, false>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+int persist_wide_rr_rot_scratch() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_wide_rr<true, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 hipError_t launch_persist_wide_rr(const PersistRRArgs& a, hipStream_t s) {
-    // full launches only (t0 = 0: the initial state is built in-kernel from k_persist_rr_init's
-    // x1, h1), RAW, 512 or 1024 classes (2 or 4 fc5 tiles of 16 per B slot)
+    // full launches (t0 = 0: the initial state is built in-kernel from k_persist_rr_init's x1,
+    // h1) or time-sliced ones (vmap: every row from its chunk state, t1 <= S steps, P1 formed
+    // in-kernel), RAW, 512 or 1024 classes (2 or 4 fc5 tiles of 16 per B slot)
     if (a.rb < 0 || a.nr < 1 || a.nr > kPWideRows || a.rb + kPG * a.nr > a.B || a.mode != 0 ||
-        a.t0 != 0 || a.t1 != a.S || (a.cpw != 32 && a.cpw != 64) || a.cpw * kHalf < a.n_classes ||
-        a.wwide == nullptr || a.wring == nullptr)
+        a.t0 != 0 || (a.vmap ? a.t1 > a.S || a.p1q == nullptr : a.t1 != a.S) || (a.cpw != 32 && a.cpw != 64) ||
+        a.cpw * kHalf < a.n_classes || a.wwide == nullptr || a.wring == nullptr)
         return hipErrorInvalidValue;
-    if (a.dbg.out) return persist_launch<k_persist_wide_rr<true>>(persist_wide_rr_lds_bytes(), a, s);
-    return persist_launch<k_persist_wide_rr<false>>(persist_wide_rr_lds_bytes(), a, s);
+    const size_t lb = persist_wide_rr_lds_bytes();
+    if (a.vmap) return a.dbg.out ? persist_launch<k_persist_wide_rr<true, true>>(lb, a, s)
+                                 : persist_launch<k_persist_wide_rr<true, false>>(lb, a, s);
+    return a.dbg.out ? persist_launch<k_persist_wide_rr<false, true>>(lb, a, s)
+                     : persist_launch<k_persist_wide_rr<false, false>>(lb, a, s);
 }
 
 // Exhaustive host check of the exchange layout (as wide_layout_check for the fatchord kernel):

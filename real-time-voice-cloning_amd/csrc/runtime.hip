@@ -2003,7 +2003,7 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
                        : rr ? std::max(persist_rr_xbuf_floats(), any_wide ? persist_wide_rr_xbuf_floats() : 0)
                             : std::max(persist_xbuf_floats(), any_wide ? persist_wide_xbuf_floats() : 0);
     CHECK(P.xbuf.alloc(xfl * sizeof(float)));
-    CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? 11 * kRH : 6 * H) * sizeof(float)));
+    CHECK(P.st.alloc((size_t)Bp * (gen ? 2 * kRH : rr ? kRRState * kRH : 6 * H) * sizeof(float)));
     // P1 (all steps, rows) was written by run_upsample next to cI; the noise by
     // persist_noise on the side stream
     const uint32_t k0 = (uint32_t)(h->seed & 0xffffffffu), k1 = (uint32_t)(h->seed >> 32);
@@ -2277,6 +2277,8 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.t1 = a.t1;
             ar.nr = a.nr;
             ar.rb = a.rb;
+            ar.rows = a.rows;  // (a time-sliced launch: its own table, and the row map)
+            ar.vmap = a.vmap;
             ar.stamps = a.stamps;
             ar.prog_base = a.prog_base;
             if (L.wide) {
@@ -2611,19 +2613,22 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         }
     }
     // time-sliced wide launches (plan_wide_slices), when cheaper than the plan
-    // above by the same cost model (fatchord RAW <= 512 classes with the in-kernel P1 ring;
-    // WRNN_PERSIST_SLICE=0 or WRNN_PERSIST_WIDE=0: off)
+    // above by the same cost model (RAW, P1 formed in-kernel: fatchord up to 1024 classes,
+    // runtimeracer; WRNN_PERSIST_SLICE=0 or WRNN_PERSIST_WIDE=0: off)
     h->wrot.clear();
-    if (h->pw.ok && !h->pw.gen && !h->pw.rr && h->pw.wwide && h->cfg.mode == WRNN_MODE_RAW && p1_ring_ok(h) &&
-        !lplan.empty()) {
+    const bool fat_sl = h->pw.ok && !h->pw.gen && !h->pw.rr && h->pw.wwide && p1_ring_ok(h);
+    const bool rr_sl = h->pw.ok && h->pw.rr && h->pw.wwide_rr && rr_frames_ok(h);
+    if ((fat_sl || rr_sl) && h->cfg.mode == WRNN_MODE_RAW && !lplan.empty()) {
         const char* e1 = std::getenv("WRNN_PERSIST_SLICE");
         const char* e2 = std::getenv("WRNN_PERSIST_WIDE");
         std::vector<wrnn_handle::WLaunch> sl;
         const bool c10 = h->n_classes > kPM * 16;
-        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && persist_wide_rot_scratch(c10) == 0 &&
+        const int rsc = fat_sl ? persist_wide_rot_scratch(c10) : persist_wide_rr_rot_scratch();
+        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && rsc == 0 &&
             plan_wide_slices(B, S, sl)) {
             double cost = 60.0 * (sl.size() - 1);  // (an extra launch: weights, ring prologue)
-            for (const auto& L : sl) cost += L.steps * (10.5 + 0.055 * L.nr + (c10 ? kWide10Us : 0.0));
+            for (const auto& L : sl)
+                cost += L.steps * (fat_sl ? 10.5 + 0.055 * L.nr + (c10 ? kWide10Us : 0.0) : kWideRRUs + 0.025 * L.nr);
             if (cost < 0.98 * plan_us * S) {
                 lplan.clear();
                 for (int j = 0; j < (int)sl.size(); ++j) lplan.push_back({0, sl[j].nr, true, j});

@@ -275,6 +275,7 @@ constexpr int kMolNoise = 12;  // floats per (step, row) of the precomputed MOL 
 constexpr int kRH = 256;     // rnn_dims == fc_dims
 constexpr int kRNR = 4;      // max fold rows per group and launch
 constexpr int kRNW = 28;     // float4 weight registers per thread
+constexpr int kRRState = 14; // chunk-state floats per row / H: x1, h1, h2, h3, h4 | gh2, gh3, gh4
 
 struct PersistRRArgs {
     unsigned* ctl;          // PC_WORDS control words
@@ -304,7 +305,8 @@ struct PersistRRArgs {
     int16_t* labels;        // [B][ld]
     float* samples;         // [B][ld]
     int ld;
-    float* st;              // chunk state [B][11 H]: x1, h1, h2, h3, h4 | gh2, gh3 (3H each)
+    float* st;              // chunk state [B][kRRState H]: x1, h1, h2, h3, h4 | gh2, gh3, gh4 (3H each;
+                            // gh4: the wide kernel's time-sliced launches only)
     uint32_t* stamps;       // optional: [0] loop start, [1] loop end (group 0, slot 0)
     unsigned* progress;     // as PersistArgs
     int prog_base;
@@ -320,6 +322,9 @@ struct PersistRRArgs {
     uint32_t k0, k1;
     uint32_t* phases;       // optional: [256][kPPhases] stamps of step phase_t (wide: slots 0, 16)
     int phase_t;
+    // time-sliced wide launch (null otherwise): virtual row v = g + 8 r ->
+    // (physical row, step offset); `rows` is then the launch's RowInfo table by virtual row
+    const int2* vmap;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
@@ -333,6 +338,7 @@ size_t persist_wide_rr_ring_floats();
 size_t persist_wide_rr_wreg_floats();
 hipError_t persist_wide_rr_reset_xbuf(float* xbuf, hipStream_t s);
 int persist_wide_rr_scratch();
+int persist_wide_rr_rot_scratch();  // the time-sliced instance (PersistRRArgs::vmap)
 int wide_rr_layout_check(int rows_per_group);
 
 // ---------------------------------------------------------------------------------------

@@ -64,3 +64,11 @@ def test_fatchord_10bit_default_batch_is_time_sliced_over_wide_launches():
     register-resident launch."""
     plan = _run('fatchord-wavernn', 'RAW', 10, 8, target=3000, overlap=1500)
     assert plan == [(0, 16, True)] * 45, plan
+
+
+def test_runtimeracer_default_batch_is_time_sliced_over_wide_launches():
+    """runtimeracer 10-bit defaults (target 6,000 / overlap 1,000) at 8 x 1000 frames: 232 rows,
+    29 per group -- 29 time-sliced wide launches (kernels_persist_wide_rr.hip) of 16 rows per
+    group x 500 steps instead of a 16-row and a 13-row launch of 8,000 steps each."""
+    plan = _run('runtimeracer-wavernn', 'RAW', 10, 8, target=6000, overlap=1000)
+    assert plan == [(0, 16, True)] * 29, plan

@@ -14,16 +14,16 @@ pytestmark = pytest.mark.gpu
 TARGET, OVERLAP = 4000, 400  # 4,800 steps (shorter calls do not pay for the extra launches)
 
 
-def _model(mode='RAW', bits=9):
+def _model(mode='RAW', bits=9, model_type='fatchord-wavernn'):
     from wavernn_amd.base import hparams_for
     from wavernn_amd.hparams import sp
     from wavernn_amd.model import WaveRNN
     from wavernn_amd.synth import synth_state_dict
-    hp = hparams_for('fatchord-wavernn').copy(bits=bits, mode=mode)
+    hp = hparams_for(model_type).copy(bits=bits, mode=mode)
     m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels, hp.compute_dims,
                 hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate, mode=mode,
-                model_type='fatchord-wavernn', device=0)
-    m.load_state_dict(synth_state_dict(hp, 'fatchord-wavernn', seed=11))
+                model_type=model_type, device=0)
+    m.load_state_dict(synth_state_dict(hp, model_type, seed=11))
     m.set_engine('persist')
     return m, hp
 
@@ -106,18 +106,20 @@ def test_rotated_call_reports_progress_at_the_reference_cadence(monkeypatch):
     assert np.array_equal(a, b_)
 
 
-@pytest.mark.parametrize('bits', [9, 10])
-def test_time_sliced_wide_equals_wide_plus_tail(bits, monkeypatch):
+@pytest.mark.parametrize('model_type,bits', [('fatchord-wavernn', 9), ('fatchord-wavernn', 10),
+                                             ('runtimeracer-wavernn', 10)])
+def test_time_sliced_wide_equals_wide_plus_tail(model_type, bits, monkeypatch):
     """8 utterances x 18 rows (the C4 shape at 4,800 steps): the time-sliced wide launches (every
     row through 16-row-per-group wide launches at its own offsets, state across launches) give
     the labels of the wide 128-row launch + register-resident 16-row launch plan
     (WRNN_PERSIST_SLICE=0) bit for bit, and so do the wide rows' logits recorded around the slice
-    boundaries (600 steps per launch at 4,800 steps: 8 of 9 launches per row). 10 bits: the
-    1024-class instances."""
+    boundaries (600 steps per launch at 4,800 steps: 8 of 9 launches per row). fatchord 10 bits:
+    the 1024-class instances; runtimeracer: the two-half kernel (kernels_persist_wide_rr.hip),
+    its four GRUs' state (and gh4) across launches."""
     import torch
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_mel
-    m, hp = _model(bits=bits)
+    m, hp = _model(bits=bits, model_type=model_type)
     T = _frames_for(m, 18)
     devs = [torch.from_numpy((synth_mel(T, 40 + u) / sp.max_abs_value).astype(np.float32)).cuda() for u in range(8)]
     steps = [0, 599, 600, 601, 1199, 1200, 2400, 4799]
