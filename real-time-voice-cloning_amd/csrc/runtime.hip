@@ -2675,7 +2675,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         h->pw.cpw <= 16 && (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL)) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
-        static const double us9[kPNR + 1] = {0, 4.8, 5.15, 5.91, 6.92};
+        // per-step rates of the rotated instance's two bodies: the (q + 1)-row one at the
+        // single-launch rate, the q-row one a little slower than its own kernel (2 rows: 5.22
+        // against 5.15 us -- the best split measured)
+        static const double us9[kPNR + 1] = {0, 4.8, 5.22, 5.91, 6.92};
         double t_hi = nr >= 1 ? us9[nr] : 0, t_lo = nr >= 2 ? us9[nr - 1] : 0;
         if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);

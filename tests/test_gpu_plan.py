@@ -37,7 +37,7 @@ def test_c2_shape_is_one_launch_of_3_rows_per_group(model_type, mode, bits):
 @pytest.mark.parametrize('mode', ['RAW', 'MOL'])
 def test_c2_fatchord_is_rotated_over_three_launches(mode, monkeypatch):
     """fatchord 9-bit at C2 (18 rows: 2 groups of 3 rows, 6 of 2): the row rotation (DESIGN.md
-    §3.0e) -- three launches, every row 3,672 steps in a 3-row group and 2 x 4,214 in 2-row
+    §3.0e) -- three launches, every row 3,706 steps in a 3-row group and 2 x 4,197 in 2-row
     groups; WRNN_PERSIST_ROT=0 restores the single launch."""
     assert _run('fatchord-wavernn', mode, 9, 1) == [(0, 3, False)] * 3
     monkeypatch.setenv('WRNN_PERSIST_ROT', '0')

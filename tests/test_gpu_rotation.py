@@ -82,8 +82,10 @@ def test_rotated_logit_capture_equals_single_launch(monkeypatch):
     from wavernn_amd.synth import synth_mel
     m, hp = _model()
     mel = synth_mel(_frames_for(m, 18), 3)
-    # around the launch boundaries (18 rows, 4,800 steps: 1,456 steps at 3 rows, 1,672 at 2)
-    steps = [0, 1455, 1456, 1672, 3128, 3129, 3344, 4799]
+    # around the launch boundaries (18 rows, 4,800 steps: n_hi steps at 3 rows, n_lo at 2; a
+    # row's offsets are 0, n_hi or n_lo, n_hi + n_lo or 2 n_lo)
+    _, (K, nh, nl), _ = _call(m, mel, monkeypatch, rot=True)
+    steps = [0, nh - 1, nh, nl, nh + nl - 1, nh + nl, 2 * nl, 4799]
     a, ra, la = _call(m, mel, monkeypatch, rot=True, debug_steps=steps)
     b, rb, lb = _call(m, mel, monkeypatch, rot=False, debug_steps=steps)
     assert ra[0] > 1 and np.array_equal(a, b)

