@@ -7,6 +7,9 @@
 #              this library's build id (bench lines then name counters of the binary they time)
 #   bench    : default line (C2, CPU baseline, parity, logit gate), counters from the pass above
 #   c4       : --utts-per-gpu 8                  rr    : runtimeracer 10-bit defaults, 8 utts
+#   b10      : fatchord 10-bit defaults (3000 / 1500), 8 utts (the 1024-class wide slices)
+# (three gpurun calls: STEPS=tests,smoke | pmc,bench,c4,rr,b10 | rehearse,phase,prof -- with
+#  WRNN_PMC_TRAFFIC pointing the later benches at the pass's pmc_traffic.json)
 #   rehearse : the N>1 path with 2 ranks on one GPU (gloo), CPU baseline + parity on rank 0
 #   phase    : C2 phase stamps                   prof  : rocprofv3 kernel-trace --stats of c2, c4, rr
 set -u
@@ -23,9 +26,10 @@ run() {  # run <name> <timeout> cmd...
   tail -3 "$O/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-S=${STEPS:-tests,smoke,pmc,bench,c4,rr,rehearse,phase,prof}
+S=${STEPS:-tests,smoke,pmc,bench,c4,rr,b10,rehearse,phase,prof}
 PT="python -u -m pytest -x -v -rA --timeout 240 --timeout-method thread"
 RR="--model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8"
+B10="--bits 10 --target 3000 --overlap 1500 --utts-per-gpu 8"
 [[ ,$S, == *,tests,* ]] && run tests 900 $PT tests -m gpu
 [[ ,$S, == *,smoke,* ]] && run smoke 300 python __graft_entry__.py smoke
 if [[ ,$S, == *,pmc,* ]]; then
@@ -34,10 +38,11 @@ if [[ ,$S, == *,pmc,* ]]; then
   python -c "import sys; sys.path[:0]=['.', 'real-time-voice-cloning_amd']; import bench; print(bench.lib_build_id())" > $P/lib_build
   B="/usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 --no-timing"
   SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-  for m in c2 c4 rr; do
+  for m in c2 c4 rr b10; do
     A=""; K="k_persist<"
-    [ $m = c4 ] && A="--utts-per-gpu 8" && K="k_persist|k_gemm"
+    [ $m = c4 ] && A="--utts-per-gpu 8" && K="k_persist_wide<"
     [ $m = rr ] && A="$RR" && K="k_persist_wide_rr"
+    [ $m = b10 ] && A="$B10" && K="k_persist_wide<"
     run ${m}_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_fetch" -o run --output-format csv -- $B $A
     run ${m}_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_write" -o run --output-format csv -- $B $A
     run ${m}_sq 240 rocprofv3 --pmc $SQ --kernel-include-regex "$K" -d "$PWD/$P/${m}_sq" -o run --output-format csv -- $B $A
@@ -48,11 +53,13 @@ fi
 [[ ,$S, == *,bench,* ]] && run bench 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 12
 [[ ,$S, == *,c4,* ]] && run c4 400 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
 [[ ,$S, == *,rr,* ]] && run rr 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 $RR
+[[ ,$S, == *,b10,* ]] && run b10 500 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 $B10
 [[ ,$S, == *,rehearse,* ]] && run rehearse 400 env WRNN_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --cpu-seconds 10
 [[ ,$S, == *,phase,* ]] && run phase 200 env WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0
 if [[ ,$S, == *,prof,* ]]; then
   run prof_c2 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_c2" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0
   run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_c4" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
   run prof_rr 400 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_rr" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 $RR
+  run prof_b10 400 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_b10" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 $B10
 fi
 exit 0

@@ -42,6 +42,9 @@ WORKLOADS = {
     'c2': ('', workload('fatchord-wavernn', 'RAW 9-bit mu-law'), 'k_persist'),
     'c4': (' --utts-per-gpu 8', workload('fatchord-wavernn', 'RAW 9-bit mu-law', utts=8), 'k_persist_wide'),
     'c3': (' --mode MOL', workload('fatchord-wavernn', 'MOL'), 'k_persist'),
+    'b10': (' --bits 10 --target 3000 --overlap 1500 --utts-per-gpu 8',
+            workload('fatchord-wavernn', 'RAW 10-bit mu-law', utts=8, target=3000, overlap=1500),
+            'k_persist_wide'),
     'rr': (' --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8',
            workload('runtimeracer-wavernn', 'RAW 10-bit mu-law', utts=8, target=6000, overlap=1000),
            'k_persist_wide_rr'),
