@@ -123,3 +123,29 @@ def test_wide_every_rows_per_group_matches_register_resident(monkeypatch):
             out[wide] = lab.cpu().numpy()
         d = np.argwhere(out['1'] != out['0'])
         assert len(d) == 0, f'R={R} ({n} rows): first divergence {d[np.argmin(d[:, 1])]}'
+
+
+@pytest.mark.parametrize('case', ['fatchord_raw9_sharp_tiny', 'fatchord_raw10_unbatched_tiny'])
+def test_wide_p1_ring_equals_stream(case, wide_only, monkeypatch):
+    """The wide kernel forms P1 in its one-slot LDS ring from the per-frame tables (p1_make) or,
+    with WRNN_P1_RING=0, copies it from k_p1_expand's [S][B][4H] stream: identical labels
+    (9-bit and the 1024-class instances)."""
+    import torch
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case(case)
+    m, hp, sd = make_model(meta)
+    m.set_engine('persist')
+    m.enable_stage_timing(True)
+    dev = [torch.from_numpy((synth_mel(meta['n_frames'], 300 + u) / sp.max_abs_value).astype(np.float32)).cuda()
+           for u in range(4)]
+    out = []
+    for ring in ('1', '0'):
+        monkeypatch.setenv('WRNN_P1_RING', ring)
+        m.set_seed(meta['noise_seed'])
+        res, roff, S = m.generate_batch_device(dev, meta['batched'], meta['target'], meta['overlap'])
+        assert _stage_names(m) == ['persist_wide']
+        out.append(res.cpu().numpy())
+    d = np.argwhere(out[0] != out[1])
+    assert len(d) == 0, f'first divergence {d[np.argmin(d[:, 1])].tolist()}'
