@@ -2218,13 +2218,21 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
         HIPC(hipMemcpyAsync(P.rot.p, h->rot_host.data(), h->rot_host.size(), hipMemcpyHostToDevice, st));
     }
     const auto t_start = std::chrono::steady_clock::now();
+    // time-sliced wide launches publish their progress on a common scale: launch b starts at the
+    // steps of the launches before it (prog_base), the host maps the total to 0 .. S
+    const bool wsl = nb > 0 && h->p_plan[0].wide && h->p_plan[0].rot >= 0;
+    long long sl_total = 0;
+    if (wsl)
+        for (const auto& L : h->p_plan) sl_total += h->wrot[L.rot].steps;
+    long long sl_cum = 0;
     for (int b = 0; b < nb; ++b) {
         const auto& L = h->p_plan[b];
         a.rb = L.rb;
         a.nr = L.nr;
         a.t0 = 0;
         a.t1 = S;
-        a.prog_base = b * S;
+        a.prog_base = wsl ? (int)sl_cum : b * S;
+        if (wsl) sl_cum += h->wrot[L.rot].steps;
         a.vmap = nullptr;
         a.gnr = a.giters = nullptr;
         a.rows = (const RowInfo*)ws.rows.p;
@@ -2337,9 +2345,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
                 }
                 if (err) break;  // failed launch: no progress to report
             }
-            const long long done = finished ? (long long)nb * S
+            const long long done = finished ? (wsl ? sl_total : (long long)nb * S)
                                             : (long long)__atomic_load_n(h->prog_host, __ATOMIC_RELAXED);
-            const long long i_done = done / nb;  // steps every row has completed
+            // steps every row has completed (sliced: the call's share of its row-steps, the
+            // launches' step total scaled to S -- the rows advance in turns, so that is the
+            // average row's step, reached by every row only at the end)
+            const long long i_done = wsl ? done * S / std::max(1LL, sl_total) : done / nb;
             while (rc == WRNN_OK && next < S && next + 1 <= i_done) {
                 const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
                 if (cb(user, (int)next, S, B, (double)(next + 1) / std::max(el, 1e-9) * B / 1000.0)) {

@@ -152,3 +152,25 @@ def test_time_sliced_wide_equals_wide_plus_tail(model_type, bits, monkeypatch):
             dd = np.abs(la[s][dr] - lb[s][dr])
             bad.append((s, len(dr), dr[:20], float(dd.max()), int((dd > 0).sum())))
     assert not bad, (bad, pa, pb)
+
+
+def test_time_sliced_call_reports_progress_in_order(monkeypatch):
+    """A time-sliced call (8 x 18 rows) with the reference's progress callback: i = 0, 100, ...
+    < S exactly once each, in order, with (S, b_size) of the call, and the labels of the call
+    without a callback (the kernels only publish a progress word)."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    T = _frames_for(m, 18)
+    devs = [torch.from_numpy((synth_mel(T, 60 + u) / sp.max_abs_value).astype(np.float32)).cuda() for u in range(8)]
+    seen = []
+    m.set_seed(5)
+    a, _, S = m.generate_batch_device(devs, True, TARGET, OVERLAP,
+                                      progress_callback=lambda i, n, b, r: seen.append((i, n, b)))
+    assert len(m.plan_info()) > 2 and all(w for _, _, w in m.plan_info())
+    m.set_seed(5)
+    b, _, _ = m.generate_batch_device(devs, True, TARGET, OVERLAP)
+    assert [s[0] for s in seen] == list(range(0, S, 100))
+    assert all(n == S and bb == 144 for _, n, bb in seen)
+    assert torch.equal(a, b)
