@@ -17,6 +17,7 @@ Shapes (BASELINE.json configs[1] and the runtimeracer fork's default topology at
   rr8   runtimeracer RAW 10-bit, 8 x 1000-frame mels, 6000 / 1000 (232 rows, wide launches);
         utterances 0 and 7 checked
   rr8pk the same with the trained-like statistics; rr8pk-reg on the register-resident kernel
+        (these two with WRNN_SWEEP_ALL=1)
 Seeds as tools/parity_sweep.py (weights 100 + case, mel 200 + case + 1000 u, noise 300 + case),
 so the round-4 sweep's recorded flips (profiles/r04/parity_sweep/) are among the cases. With
 WRNN_SWEEP_OUT set, one JSON line per utterance is appended there (DESIGN.md §5 numbers).
@@ -43,7 +44,12 @@ SHAPES = {
     'rr8pk-reg': dict(topo='runtimeracer', bits=10, target=6000, overlap=1000, utts=8,
                       stats=dict(gru_scale=3.0, fc_scale=2.0, logit_scale=16.0), wide='0'),
 }
-CASES = [(shape, case) for shape in SHAPES for case in range(2 if shape.startswith('rr8pk') else 4)]
+# the gate (>= 4 seed triples x {C2 default, C2 trained-like, runtimeracer 8
+# utterances}); WRNN_SWEEP_ALL=1 adds the trained-like runtimeracer cases on both kernels (the
+# DESIGN.md §5 table; ~95 s more)
+_ALL = os.environ.get('WRNN_SWEEP_ALL') == '1'
+CASES = [(shape, case) for shape in SHAPES for case in range(2 if shape.startswith('rr8pk') else 4)
+         if _ALL or not shape.startswith('rr8pk')]
 
 
 def _build(shape, case):
