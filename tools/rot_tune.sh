@@ -1,11 +1,11 @@
 # Rotation balance A/B: the C2 call time for planner rates WRNN_ROT_US="t_hi,t_lo" (µs per step of
-# the 3-row / 2-row groups), interleaved rounds
+# the 3-row / 2-row groups), interleaved rounds (BENCH_ARGS: e.g. --mode MOL; TAGS: log name suffix)
 set -u
 mkdir -p gpurun_out/rot
 for r in 1 2; do
   for rates in ${RATES:-"5.91,5.22" "5.91,5.28" "5.91,5.35" "5.91,5.42"}; do
-    WRNN_ROT_US=$rates timeout -k 10 120 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/rot/$rates.r$r.log 2>&1 || { echo "fail $rates"; exit 1; }
-    python - gpurun_out/rot/$rates.r$r.log "$rates" <<'PY'
+    WRNN_ROT_US=$rates timeout -k 10 120 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/rot/$rates${TAGS:-}.r$r.log 2>&1 || { echo "fail $rates"; exit 1; }
+    python - gpurun_out/rot/$rates${TAGS:-}.r$r.log "$rates${TAGS:-}" <<'PY'
 import json,sys
 for l in open(sys.argv[1]):
     if l.startswith('{'):
