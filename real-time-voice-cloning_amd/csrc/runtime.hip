@@ -2691,6 +2691,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         // against 5.15 us -- the best split measured)
         static const double us9[kPNR + 1] = {0, 4.8, 5.22, 5.91, 6.92};
         double t_hi = nr >= 1 ? us9[nr] : 0, t_lo = nr >= 2 ? us9[nr - 1] : 0;
+        // MOL: its rotated 3-row body (one spilled register) runs much slower than the 2-row
+        // one -- the split balanced for 5.91 / 4.70 is the fastest of a scan from 5.22 down to
+        // 4.55 (C3 5.61 -> 5.19 us per step; DESIGN.md §3.0e, profiles/r05/rotation/)
+        if (h->cfg.mode == WRNN_MODE_MOL && nr == 3) t_lo = 4.70;
         if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
