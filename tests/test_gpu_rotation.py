@@ -174,3 +174,47 @@ def test_time_sliced_call_reports_progress_in_order(monkeypatch):
     assert [s[0] for s in seen] == list(range(0, S, 100))
     assert all(n == S and bb == 144 for _, n, bb in seen)
     assert torch.equal(a, b)
+
+
+def test_time_sliced_ragged_utterances_equal_unsliced(monkeypatch):
+    """Eight utterances of different lengths (17-20 fold rows each, 144 in all: ragged tail folds,
+    rows of one utterance in several groups) through the time-sliced wide launches: labels equal
+    the unsliced plan's bit for bit, utterance by utterance."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    counts = [17, 19, 18, 18, 20, 16, 18, 18]
+    devs = [torch.from_numpy((synth_mel(_frames_for(m, c), 80 + u) / sp.max_abs_value).astype(np.float32)).cuda()
+            for u, c in enumerate(counts)]
+    res = {}
+    for sl in ('1', '0'):
+        monkeypatch.setenv('WRNN_PERSIST_SLICE', sl)
+        m.set_seed(21)
+        out, roff, S = m.generate_batch_device(devs, True, TARGET, OVERLAP)
+        res[sl] = (out.cpu().numpy(), list(roff), m.plan_info())
+    (a, ra, pa), (b, rb, pb) = res['1'], res['0']
+    assert ra == rb and ra[-1] == 144 and len(pa) > 2 and all(w for _, _, w in pa), (ra, pa)
+    for u in range(len(counts)):
+        d = np.argwhere(a[ra[u]:ra[u + 1]] != b[rb[u]:rb[u + 1]])
+        assert len(d) == 0, f'utterance {u}: first difference {d[np.argmin(d[:, 1])].tolist()}'
+
+
+def test_rotated_ragged_utterances_equal_single_launch(monkeypatch):
+    """Two utterances of 9 and 8 fold rows (17 rows: one group of 3, seven of 2) rotated: labels
+    equal the single launch's."""
+    import torch
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model()
+    devs = [torch.from_numpy((synth_mel(_frames_for(m, c), 90 + u) / sp.max_abs_value).astype(np.float32)).cuda()
+            for u, c in enumerate((9, 8))]
+    res = {}
+    for rot in ('1', '0'):
+        monkeypatch.setenv('WRNN_PERSIST_ROT', rot)
+        m.set_seed(23)
+        out, roff, S = m.generate_batch_device(devs, True, TARGET, OVERLAP)
+        res[rot] = (out.cpu().numpy(), m.rot_info())
+    assert res['1'][1][0] > 1 and res['0'][1][0] == 0, (res['1'][1], res['0'][1])
+    d = np.argwhere(res['1'][0] != res['0'][0])
+    assert len(d) == 0, f'first difference {d[np.argmin(d[:, 1])].tolist()}'
