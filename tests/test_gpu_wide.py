@@ -79,7 +79,7 @@ def test_wide_row_counts_match_oracle(n_utts, wide_only):
 
 
 def test_default_plan_uses_wide_launch_for_c4_rows():
-    """144 rows (C4 per GPU) -> one wide launch of 128 rows + one register-resident launch."""
+    """144 rows (C4 per GPU) -> wide launches (time-sliced since round 5)."""
     import torch
     from test_gpu_parity import make_model
     from wavernn_amd.hparams import sp
@@ -149,3 +149,34 @@ def test_wide_p1_ring_equals_stream(case, wide_only, monkeypatch):
         out.append(res.cpu().numpy())
     d = np.argwhere(out[0] != out[1])
     assert len(d) == 0, f'first divergence {d[np.argmin(d[:, 1])].tolist()}'
+
+
+def test_wide_10bit_time_sliced_batch_matches_oracle():
+    """fatchord 10-bit (1024 classes) at target 3000 / overlap 1500, 8 utterances of 17 fold rows
+    (136 rows, 17 per group): 17 time-sliced wide launches of 16 rows per group x 375 steps on the
+    1024-class instances (each row in 16 of them, its state carried across); utterances 0 and 7
+    against the oracle, every label of all 6,000 steps."""
+    import torch
+    from oracle.wavernn_oracle import oracle_infer_waveform
+    from test_gpu_parity import make_model
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.synth import synth_mel
+    meta, _ = golden_case('fatchord_raw10_defaults')
+    m, hp, sd = make_model(meta)
+    T = next(t for t in range(2, 2000) if m.fold_shape(t, True, 3000, 1500)[0] == 17)
+    mels = [synth_mel(T, 700 + u) / sp.max_abs_value for u in range(8)]
+    dev = [torch.from_numpy(x.astype(np.float32)).cuda() for x in mels]
+    m.set_engine('persist')
+    m.set_seed(meta['noise_seed'])
+    m.enable_stage_timing(True)
+    lab, roff, S = m.generate_batch_device(dev, True, 3000, 1500)
+    plan = m.plan_info()
+    assert roff[-1] == 136 and S == 6000 and plan == [(0, 16, True)] * 17, (roff, S, plan)
+    lab = lab.cpu().numpy()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    for u in (0, 7):
+        ref = oracle_infer_waveform(sd, hp, meta['model_type'], mels[u] * sp.max_abs_value,
+                                    target=3000, overlap=1500, seed=meta['noise_seed'], stream=u)
+        got = lab[roff[u]:roff[u + 1]]
+        d = np.argwhere(got != ref['labels'])
+        assert len(d) == 0, f'utt {u}: first divergence {d[np.argmin(d[:, 1])].tolist() if len(d) else None}'
