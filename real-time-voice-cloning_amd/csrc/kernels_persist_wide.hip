@@ -186,9 +186,10 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 //      steps [0, t1) of its rows (their steps off .. off + t1 - 1) and saves their state at the end
 // C10: up to 1024 classes (fatchord's 10-bit default): slot w also owns classes 512 + 16 w ..
 //      512 + 16 w + 15, a second fc3 tile whose A operands (a.wfc3b, 1 MiB per group image,
-//      L2-resident) are loaded every step in the hop-C wait -- the registers hold the other nine
-//      tiles; its partials go to PH after one more barrier (the gh1 / gh2 partial sums are read
-//      in the hop-C wait instead of hop D, so PH is free by then)
+//      L2-resident) are loaded every step right after the hop-C poll and consumed after the
+//      first tile's MFMAs -- the registers hold the other nine tiles; its partials go to PH after
+//      one more barrier (the gh1 / gh2 partial sums are read in the hop-C wait instead of hop D,
+//      so PH is free by then)
 #ifndef WRNN_FC3B_POL
 #define WRNN_FC3B_POL 0  // cache policy of the second fc3 tile's loads (A/B: 2 = non-temporal)
 #endif
