@@ -1,7 +1,8 @@
 """The wide-row persistent launch (kernels_persist_wide.hip: 16 rows per XCD group, fp32 MFMA
 products, distributed GRU1, five hops per step) against the reference's golden outputs and the
 oracle. ``WRNN_PERSIST_WIDE=1`` makes every launch of a call wide (1..16 rows per group);
-the default plan mixes wide and register-resident launches by cost (C4: 128 + 16 rows).
+the default plan picks wide, register-resident or time-sliced wide launches by cost (C4: 11
+time-sliced wide launches of 16 rows per group).
 
 Reference step: vocoder/models/fatchord_version.py:192-236; bar: bit-exact 9-bit labels.
 """
