@@ -66,7 +66,8 @@ constexpr int L_SX = L_RED + 32 * kRNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 8;
 constexpr int L_DUMMY = L_SX + 12;               // sink of padding poll lanes (float2)
 constexpr int L_RI = L_SX + 16;                  // RowInfo of the group's rows
-constexpr int L_CB = L_RI + 6 * kRNR + 4;        // slot constants, see CB_*
+constexpr int L_VM = L_RI + 6 * kRNR;            // (physical row, step offset) per row slot (rotated)
+constexpr int L_CB = L_VM + 2 * kRNR + 4;        // slot constants, see CB_*
 constexpr int CB_IH2 = 0, CB_IH4 = 24, CB_HH1 = 48, CB_HH2 = 72, CB_HH3 = 96, CB_HH4 = 120,
               CB_F2 = 144, CB_F4 = 152;
 constexpr int L_W5 = L_CB + 160;                 // fc5 rows of the slot [32][RH]
@@ -179,23 +180,17 @@ __device__ __forceinline__ bool poll_hop_hx(rsrc_t xr, unsigned so, unsigned seq
 }  // namespace
 
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-template <int NR, bool MOL, bool DBG>
-__global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_group, s_slot, s_ok;
+// ROT: a rotated launch (PersistRRArgs::vmap, DESIGN.md §3.0e, as kernels_persist.hip): row
+//      slot r of the group is the virtual row g + 8 r, mapped to (physical row, step offset);
+//      the group runs a.giters[g] steps from its rows' chunk state and saves it at the end; P1
+//      and the noise are read at the row's own step, labels / logits written there.
+template <int NR, bool MOL, bool ROT, bool DBG>
+__device__ __forceinline__ void rr_body(const PersistRRArgs& a, float* lds, const int g, const int w) {
+    static_assert(!(ROT && MOL), "rotated runtimeracer launches are RAW");
     const int tid = threadIdx.x;
-    // ---- group formation (as kernels_persist.hip) -------------------------------------------
-    if (tid == 0) {
-        int gg, ss;
-        s_ok = p_register(a.ctl, gg, ss);
-        s_group = gg;
-        s_slot = ss;
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const int g = __builtin_amdgcn_readfirstlane(s_group);
-    const int w = __builtin_amdgcn_readfirstlane(s_slot);
-    const int g0 = a.rb + g;                  // first fold row of this group in this launch
+    const int g0 = a.rb + g;                  // first (virtual) fold row of this group in this launch
+    const int t1g = ROT ? __builtin_amdgcn_readfirstlane(a.giters[g]) : a.t1;
+    auto vmap_g = [&](int r) -> int2 { return ROT ? a.vmap[g0 + kPG * r] : make_int2(g0 + kPG * r, 0); };
     const int q = tid >> 7;                   // quad (wave-uniform)
     const int og = (tid >> 4) & 7, kc = tid & 15;
     const int u = RU * w + og;                // unit / output of this thread's weight rows
@@ -230,7 +225,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
         const int r = 2 * i + hs;
         h1[i] = 0.f;
         if (r < NR) {
-            const float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+            const float* st = a.st + (size_t)vmap_g(r).x * SW;
             h1[i] = st[RH + j];
             lds[L_XA + r * RH + j] = st[j];
             lds[L_H1 + r * RH + j] = h1[i];
@@ -239,7 +234,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     }
     const bool own = kc < NR;  // lane kc owns (unit u, row kc) in the epilogues
     const int lr = own ? kc : 0;
-    const int lrow = g0 + kPG * lr;
+    const int2 lvm = vmap_g(lr);  // (physical row, step offset) of this lane's epilogue row
+    const int lrow = lvm.x;
     float h2r = 0.f, h3r = 0.f, h4r = 0.f;
     if (own) {
         const float* st = a.st + (size_t)lrow * SW;
@@ -268,7 +264,10 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             lds[L_CB + CB_F4 + tid] = a.b_f4[RU * w + tid];
         }
     }
-    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid < NR) {
+        reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+        reinterpret_cast<int2*>(lds + L_VM)[tid] = vmap_g(tid);
+    }
     if (tid == 0) lds[L_FAIL] = 0.f;
     const float vj0 = a.v[j], vj1 = a.v[RH + j], vj2 = a.v[2 * RH + j], w0j = a.w0[j];
     const float bcls = has_cls ? a.b_f5[cls] : 0.f;
@@ -287,7 +286,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     auto sf = [](int k) { return (unsigned)(RX_F + k * RX_F_SZ) * 4u; };
 
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
-    for (int t = a.t0; t < a.t1; ++t) {
+    for (int t = a.t0; t < t1g; ++t) {
         const unsigned seq = (unsigned)t + 1u;
         const bool nxt = t + 1 < a.S;
         const unsigned par = (unsigned)(t & 1);
@@ -454,8 +453,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
                 if (r < NR) {
-                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
-                        pr, o_tid * 4u, (unsigned)(r * kPG * 4 * RH) * 4u, 0);
+                    u4v v;
+                    if constexpr (ROT) {  // row r (wave-uniform) at its own step, clamped to S - 1
+                        const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                        const int px = __builtin_amdgcn_readfirstlane(vm.x), po = __builtin_amdgcn_readfirstlane(vm.y);
+                        const int ts = t + 1 + po < a.S ? t + 1 + po : a.S - 1;
+                        v = __builtin_amdgcn_raw_buffer_load_b128(
+                            mk_rsrc(a.P1 + ((size_t)ts * a.B + px) * 4 * RH), o_tid * 4u, 0, 0);
+                    } else {
+                        v = __builtin_amdgcn_raw_buffer_load_b128(pr, o_tid * 4u, (unsigned)(r * kPG * 4 * RH) * 4u, 0);
+                    }
                     pP[i][0] = __uint_as_float(v.x);
                     pP[i][1] = __uint_as_float(v.y);
                     pP[i][2] = __uint_as_float(v.z);
@@ -464,9 +471,15 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             }
         }
         float pgum = 0.f;  // Gumbel noise of (row kc, class cls), step t
-        if (own && has_cls && !MOL)
-            pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
-                       (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+        if (own && has_cls && !MOL) {
+            if constexpr (ROT)  // (the row's own step; the stream < 4 GiB, runtime-checked)
+                pgum = bld(mk_rsrc(a.gumbel),
+                           (unsigned)((((unsigned)(t + lvm.y) * (unsigned)a.B + (unsigned)lrow) * (unsigned)a.n_classes +
+                                       (unsigned)cls) * 4u), 0);
+            else
+                pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
+                           (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+        }
         // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
         if (MOL && tid < 32 * NR && (tid & 31) < 11)
             pgum = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + g0 + kPG * (tid >> 5)) * kMolNoise),
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 float l = -INFINITY;
                 if (has_cls) {
                     l = p_add(s0, bcls);
-                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t + (ROT ? lvm.y : 0), lrow, cls, a.B, a.n_classes, l);
                 }
                 *reinterpret_cast<float2*>(red + (cl * kRNR + kc) * 2) = make_float2(l, pgum);
             }
@@ -631,7 +644,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                     }
                     lds[L_SX + r] = xv;
                     if (w == 0) {
-                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        if (ROT) {
+                            const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                            ro = (unsigned)(vm.x * a.ld + vm.y);
+                        }
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
                                                               ro * 2u, (unsigned)t * 2u, 0);
                         bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -708,7 +725,8 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
             }
         }
         if (w == 0 && tid == 0) {
-            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            // (rotated: the launch's share of the call, steps scaled to S per launch)
+            if (g == 0) p_progress(a.progress, a.prog_base, ROT ? (int)((long long)t * a.S / t1g) : t, t);
             if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next step's check
         }
         __syncthreads();
@@ -716,17 +734,17 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
     // ---- save the chunk state ----------------------------------------------------------------
     // (lane indices recomputed here: values kept alive across the step loop cost registers)
-    if (a.t1 < a.S) {
+    if (ROT || a.t1 < a.S) {
         int tx = tid;
         asm volatile("" : "+v"(tx));
         const int jx = tx & (RH - 1), hx = tx >> 8, kx = tx & 15;
-        const int ux = RU * w + ((tx >> 4) & 7), rx = g0 + kPG * (kx < NR ? kx : 0);
+        const int ux = RU * w + ((tx >> 4) & 7), rx = vmap_g(kx < NR ? kx : 0).x;
         if (w == 0)
 #pragma unroll
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hx;
                 if (r < NR) {
-                    float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+                    float* st = a.st + (size_t)vmap_g(r).x * SW;
                     st[jx] = lds[L_XA + r * RH + jx];
                     st[RH + jx] = lds[L_H1 + r * RH + jx];
                 }
@@ -745,7 +763,33 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
                 st[4 * RH + ux] = h4r;
             }
         }
-    }}
+    }
+}
+
+template <int NR, bool MOL, bool ROT, bool DBG>
+__global__ __launch_bounds__(kPT, 1) void k_persist_rr(PersistRRArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    // ---- group formation (as kernels_persist.hip) -------------------------------------------
+    if (threadIdx.x == 0) {
+        int gg, ss;
+        s_ok = p_register(a.ctl, gg, ss);
+        s_group = gg;
+        s_slot = ss;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    if constexpr (ROT && NR >= 2) {  // each group runs its own row count's body
+        if (__builtin_amdgcn_readfirstlane(a.gnr[g]) == NR)
+            rr_body<NR, MOL, true, DBG>(a, lds, g, w);
+        else
+            rr_body<NR - 1, MOL, true, DBG>(a, lds, g, w);
+    } else {
+        rr_body<NR, MOL, false, DBG>(a, lds, g, w);
+    }
+}
 
 // Step-0 state: GRU1 with x = 0, h = 0 (gh = b_hh1) -> x1(0), h1(0); h2 = h3 = h4 = 0,
 // gh2 = b_hh2, gh3 = b_hh3, gh4 = b_hh4.
@@ -778,14 +822,30 @@ size_t persist_rr_xbuf_floats() { return (size_t)kPG * RX_GROUP; }
 
 template <int NR, bool MOL>
 hipError_t launch_persist_rr_t(const PersistRRArgs& a, hipStream_t s) {
-    if (a.dbg.out) return persist_launch<k_persist_rr<NR, MOL, true>>(persist_rr_lds_bytes(), a, s);
-    return persist_launch<k_persist_rr<NR, MOL, false>>(persist_rr_lds_bytes(), a, s);
+    if constexpr (!MOL && NR >= 2) {
+        if (a.vmap) {  // rotated (RAW, 2-4 rows per group)
+            if (a.dbg.out) return persist_launch<k_persist_rr<NR, MOL, true, true>>(persist_rr_lds_bytes(), a, s);
+            return persist_launch<k_persist_rr<NR, MOL, true, false>>(persist_rr_lds_bytes(), a, s);
+        }
+    }
+    if (a.vmap) return hipErrorInvalidValue;
+    if (a.dbg.out) return persist_launch<k_persist_rr<NR, MOL, false, true>>(persist_rr_lds_bytes(), a, s);
+    return persist_launch<k_persist_rr<NR, MOL, false, false>>(persist_rr_lds_bytes(), a, s);
 }
 
 template <int NR, bool MOL>
 int persist_rr_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL, false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL, false, false>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+// scratch bytes of the rotated RAW instance of nr (2-4) rows per group; -1 if none
+int persist_rr_rot_scratch(int nr) {
+    hipFuncAttributes fa;
+    const void* f = nr == 2 ? (const void*)k_persist_rr<2, false, true, false>
+                  : nr == 3 ? (const void*)k_persist_rr<3, false, true, false>
+                  : nr == 4 ? (const void*)k_persist_rr<4, false, true, false> : nullptr;
+    if (!f || hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 

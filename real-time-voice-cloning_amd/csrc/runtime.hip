@@ -2285,8 +2285,10 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ar.t1 = a.t1;
             ar.nr = a.nr;
             ar.rb = a.rb;
-            ar.rows = a.rows;  // (a time-sliced launch: its own table, and the row map)
+            ar.rows = a.rows;  // (a time-sliced / rotated launch: its own table, and the row map)
             ar.vmap = a.vmap;
+            ar.gnr = a.gnr;
+            ar.giters = a.giters;
             ar.stamps = a.stamps;
             ar.prog_base = a.prog_base;
             if (L.wide) {
@@ -2682,8 +2684,15 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // row rotation (plan_rotation): one register-resident 9-bit launch with
     // uneven groups becomes K launches over rotating row sets (WRNN_PERSIST_ROT=0: off)
     h->rot_plan = wrnn_handle::RotPlan();
-    if (use_p && h->p1_ring && h->p_plan.size() == 1 && !h->p_plan[0].wide && !h->pw.rr && !h->pw.gen &&
-        h->pw.cpw <= 16 && (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL)) {
+    const bool fat_rot = use_p && h->p1_ring && h->p_plan.size() == 1 && !h->p_plan[0].wide && !h->pw.rr &&
+                         !h->pw.gen && h->pw.cpw <= 16 &&
+                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
+    // runtimeracer (k_persist_rr, RAW): P1 and the noise from their streams at each row's own
+    // step (the noise stream addressed with 32-bit offsets: < 4 GiB)
+    const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
+                        h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
+                        (double)S * B * h->n_classes * 4.0 < 4.0e9;
+    if (fat_rot || rr_rot) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
         // per-step rates of the rotated instance's two bodies: the (q + 1)-row one at the
@@ -2695,11 +2704,18 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         // one -- the split balanced for 5.91 / 4.70 is the fastest of a scan from 5.22 down to
         // 4.55 (C3 5.61 -> 5.19 us per step; DESIGN.md §3.0e, profiles/r05/rotation/)
         if (h->cfg.mode == WRNN_MODE_MOL && nr == 3) t_lo = 4.70;
+        if (rr_rot) {  // runtimeracer, measured single-launch step times at 1-4 rows per group
+            static const double rr9[kPNR + 1] = {0, 6.3, 7.0, 7.78, 8.8};   // 9-bit (2 / 4 rows: estimates)
+            static const double rr10[kPNR + 1] = {0, 6.5, 7.26, 8.14, 9.23};  // 10-bit (profiles/r05/rr_rates/)
+            const double* us = h->pw.cpw > 16 ? rr10 : rr9;
+            t_hi = us[nr];
+            t_lo = us[nr - 1];
+        }
         if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
-        const int rs = nr >= 2 ? persist_rot_scratch(nr, h->cfg.mode) : -1;
+        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr) : persist_rot_scratch(nr, h->cfg.mode);
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
             plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
             h->p_plan.clear();

@@ -322,12 +322,16 @@ struct PersistRRArgs {
     uint32_t k0, k1;
     uint32_t* phases;       // optional: [256][kPPhases] stamps of step phase_t (wide: slots 0, 16)
     int phase_t;
-    // time-sliced wide launch (null otherwise): virtual row v = g + 8 r ->
-    // (physical row, step offset); `rows` is then the launch's RowInfo table by virtual row
+    // time-sliced wide launch or rotated register-resident launch (§3.0e; null
+    // otherwise): virtual row v = g + 8 r -> (physical row, step offset); `rows` is then the
+    // launch's RowInfo table by virtual row; rotated: rows and steps per group
     const int2* vmap;
+    const int* gnr;
+    const int* giters;
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
+int persist_rr_rot_scratch(int nr);  // the rotated RAW instance's scratch bytes (-1: none)
 // Wide-row runtimeracer launch (kernels_persist_wide_rr.hip): up to kPWideRows rows per XCD
 // group, the group split into two halves of 16 slots that own 16 units of alternate layers,
 // fp32 MFMA products, RAW categorical with 512 or 1024 classes (cpw = n / 16 per B slot).

@@ -218,3 +218,24 @@ def test_rotated_ragged_utterances_equal_single_launch(monkeypatch):
     assert res['1'][1][0] > 1 and res['0'][1][0] == 0, (res['1'][1], res['0'][1])
     d = np.argwhere(res['1'][0] != res['0'][0])
     assert len(d) == 0, f'first difference {d[np.argmin(d[:, 1])].tolist()}'
+
+
+@pytest.mark.parametrize('bits,rows', [(9, 18), (10, 20), (9, 17)])
+def test_rotated_runtimeracer_labels_equal_single_launch(bits, rows, monkeypatch):
+    """The runtimeracer register-resident kernel rotated (k_persist_rr<..., ROT>: rows at their
+    own step offsets, the four GRUs' chunk state across launches, P1 and the noise streams read
+    at each row's own step): labels, and the logits recorded around the launch boundaries, equal
+    the single launch's bit for bit."""
+    from wavernn_amd.synth import synth_mel
+    m, hp = _model(bits=bits, model_type='runtimeracer-wavernn')
+    mel = synth_mel(_frames_for(m, rows), 600 + rows)
+    _, (K, nh, nl), _ = _call(m, mel, monkeypatch, rot=True)
+    steps = [0, nh - 1, nh, nl, nh + nl - 1, nh + nl, 2 * nl, 4799]
+    a, ra, la = _call(m, mel, monkeypatch, rot=True, debug_steps=steps)
+    b, rb, lb = _call(m, mel, monkeypatch, rot=False, debug_steps=steps)
+    assert a.shape[0] == rows and ra[0] > 1 and rb[0] == 0, (a.shape, ra, rb)
+    d = np.argwhere(a != b)
+    assert len(d) == 0, f'{rows} rows: first difference {d[np.argmin(d[:, 1])].tolist()}'
+    for s in steps:
+        assert np.isfinite(la[s]).all(), s
+        assert np.array_equal(la[s], lb[s]), s
