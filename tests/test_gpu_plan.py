@@ -28,10 +28,16 @@ def _run(model_type, mode, bits, n_utts, frames=1000, target=11000, overlap=550)
     return m.plan_info()
 
 
-@pytest.mark.parametrize('model_type,mode,bits', [('runtimeracer-wavernn', 'RAW', 9),
-                                                  ('geneing-wavernn', 'BITS', 10)])
-def test_c2_shape_is_one_launch_of_3_rows_per_group(model_type, mode, bits):
-    assert _run(model_type, mode, bits, 1) == [(0, 3, False)]
+def test_c2_shape_geneing_is_one_launch_of_3_rows_per_group():
+    assert _run('geneing-wavernn', 'BITS', 10, 1) == [(0, 3, False)]
+
+
+def test_c2_shape_runtimeracer_is_rotated_over_three_launches(monkeypatch):
+    """runtimeracer 9-bit at C2 (18 rows): the rotated k_persist_rr, three
+    launches of 3 / 2 rows per group; WRNN_PERSIST_ROT=0 restores the single 3-row launch."""
+    assert _run('runtimeracer-wavernn', 'RAW', 9, 1) == [(0, 3, False)] * 3
+    monkeypatch.setenv('WRNN_PERSIST_ROT', '0')
+    assert _run('runtimeracer-wavernn', 'RAW', 9, 1) == [(0, 3, False)]
 
 
 @pytest.mark.parametrize('mode', ['RAW', 'MOL'])
