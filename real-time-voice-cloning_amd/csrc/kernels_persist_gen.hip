@@ -52,9 +52,10 @@ constexpr int L_SX = L_RED + 32 * GNR * 2;
 constexpr int L_FAIL = L_SX + 8;
 constexpr int L_DUMMY = L_SX + 12;
 constexpr int L_RI = L_SX + 16;
-constexpr int L_CB = L_RI + 6 * GNR + 4;       // b_hh1 of the slot's units [3][8]
+constexpr int L_VM = L_RI + 6 * GNR + 4;       // (physical row, step offset) per row slot (rotated)
+constexpr int L_CB = L_VM + 2 * GNR + 4;       // b_hh1 of the slot's units [3][8]
 constexpr int L_TOTAL = L_CB + 24;
-static_assert(L_DUMMY % 2 == 0, "float2 sink");
+static_assert(L_DUMMY % 2 == 0 && L_VM % 2 == 0, "float2 sink, int2 row map");
 
 // poll NPAIR tagged pairs per row x NR rows into LDS dst[r * NPAIR + ...]
 template <int NR, int NPAIR>
@@ -81,23 +82,17 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
 
 // MODE: 0 RAW (categorical, 'BITS'), 1 MOL, 2 BETA (geneing 'RAW'); each its own instantiation
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
-template <int NR, int MODE, bool DBG>
-__global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_group, s_slot, s_ok;
+// ROT: a rotated launch (PersistGenArgs::vmap, DESIGN.md §3.0e, as kernels_persist_rr.hip): row
+//      slot r of the group is the virtual row g + 8 r, mapped to (physical row, step offset);
+//      the group runs a.giters[g] steps from its rows' chunk state and saves it at the end; P1
+//      and the noise are read at the row's own step, labels / logits written there.
+template <int NR, int MODE, bool ROT, bool DBG>
+__device__ __forceinline__ void gen_body(const PersistGenArgs& a, float* lds, const int g, const int w) {
+    static_assert(!(ROT && MODE != 0), "rotated geneing launches are RAW");
     const int tid = threadIdx.x;
-    // ---- group formation (as kernels_persist.hip) -------------------------------------------
-    if (tid == 0) {
-        int gg, ss;
-        s_ok = p_register(a.ctl, gg, ss);
-        s_group = gg;
-        s_slot = ss;
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const int g = __builtin_amdgcn_readfirstlane(s_group);
-    const int w = __builtin_amdgcn_readfirstlane(s_slot);
     const int g0 = a.rb + g;
+    const int t1g = ROT ? __builtin_amdgcn_readfirstlane(a.giters[g]) : a.t1;
+    auto vmap_g = [&](int r) -> int2 { return ROT ? a.vmap[g0 + kPG * r] : make_int2(g0 + kPG * r, 0); };
     const int q = tid >> 7;
     const int og = (tid >> 4) & 7, kc = tid & 15;
     const int u = GU * w + og;                  // GRU unit of quad 0's weight rows
@@ -122,18 +117,22 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
         const int r = 2 * i + hs;
         h1[i] = 0.f;
         if (r < NR) {
-            const float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+            const float* st = a.st + (size_t)vmap_g(r).x * SW;
             h1[i] = st[GH + j];
             lds[L_XA + r * GH + j] = st[j];
             lds[L_H1 + r * GH + j] = h1[i];
         }
     }
     if (tid < 24) lds[L_CB + tid] = a.b_hh1[(tid >> 3) * GH + GU * w + (tid & 7)];
-    if (tid < NR) reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+    if (tid < NR) {
+        reinterpret_cast<RowInfo*>(lds + L_RI)[tid] = a.rows[g0 + kPG * tid];
+        reinterpret_cast<int2*>(lds + L_VM)[tid] = vmap_g(tid);
+    }
     if (tid == 0) lds[L_FAIL] = 0.f;
     const bool own = kc < NR;
     const int lr = own ? kc : 0;
-    const int lrow = g0 + kPG * lr;
+    const int2 lvm = vmap_g(lr);  // (physical row, step offset) of this lane's epilogue row
+    const int lrow = lvm.x;
     const float vj0 = a.v[j], vj1 = a.v[GH + j], vj2 = a.v[2 * GH + j], w0j = a.w0[j];
     const float bcls = has_cls ? a.b_f3[cls] : 0.f;
     const rsrc_t fcr = mk_rsrc(a.fcond);
@@ -147,18 +146,25 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
     const int wave = tid >> 6;
 
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[0] = p_now();
-    for (int t = a.t0; t < a.t1; ++t) {
+    for (int t = a.t0; t < t1g; ++t) {
         const unsigned seq = (unsigned)t + 1u;
         const bool nxt = t + 1 < a.S;
         // ---- per-step loads: fc1 conditioning, noise, P1 / cI of step t+1 -------------------
+        // (rotated: the RowInfo table by virtual row carries the row's offset in rel0)
         float pc = 0.f, pgum = 0.f;
         if (own) {
             const RowInfo& lri = reinterpret_cast<const RowInfo*>(lds + L_RI)[kc];
             if (q == 1 && og < GO)
                 pc = bld(fcr, (unsigned)(p_frame(lri, t, a.hop) * a.cond_width + a.oF1 + o) * 4u, 0);
-            if (has_cls && MODE == 0)
-                pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
-                           (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+            if (has_cls && MODE == 0) {
+                if constexpr (ROT)  // (the row's own step; the stream < 4 GiB, runtime-checked)
+                    pgum = bld(mk_rsrc(a.gumbel),
+                               (unsigned)((((unsigned)(t + lvm.y) * (unsigned)a.B + (unsigned)lrow) * (unsigned)a.n_classes +
+                                           (unsigned)cls) * 4u), 0);
+                else
+                    pgum = bld(mk_rsrc(a.gumbel + (size_t)t * a.B * a.n_classes),
+                               (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
+            }
         }
         // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
         if (MODE == 1 && tid < 32 * NR && (tid & 31) < 11)
@@ -173,8 +179,16 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             for (int i = 0; i < NRH; ++i) {
                 const int r = 2 * i + hs;
                 if (r < NR) {
-                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(
-                        pr, o_tid * 4u, (unsigned)(r * kPG * 4 * GH) * 4u, 0);
+                    u4v v;
+                    if constexpr (ROT) {  // row r (wave-uniform) at its own step, clamped to S - 1
+                        const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                        const int px = __builtin_amdgcn_readfirstlane(vm.x), po = __builtin_amdgcn_readfirstlane(vm.y);
+                        const int ts = t + 1 + po < a.S ? t + 1 + po : a.S - 1;
+                        v = __builtin_amdgcn_raw_buffer_load_b128(
+                            mk_rsrc(a.P1 + ((size_t)ts * a.B + px) * 4 * GH), o_tid * 4u, 0, 0);
+                    } else {
+                        v = __builtin_amdgcn_raw_buffer_load_b128(pr, o_tid * 4u, (unsigned)(r * kPG * 4 * GH) * 4u, 0);
+                    }
                     pP[i][0] = __uint_as_float(v.x);
                     pP[i][1] = __uint_as_float(v.y);
                     pP[i][2] = __uint_as_float(v.z);
@@ -249,7 +263,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                 float l = -INFINITY;
                 if (has_cls) {
                     l = p_add(s0, bcls);
-                    p_dbg_logit<DBG>(a.dbg, t, g0 + kPG * kc, cls, a.B, a.n_classes, l);
+                    p_dbg_logit<DBG>(a.dbg, t + lvm.y, lrow, cls, a.B, a.n_classes, l);
                 }
                 *reinterpret_cast<float2*>(red + (cl * GNR + kc) * 2) = make_float2(l, pgum);
             }
@@ -333,7 +347,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
                     }
                     lds[L_SX + r] = xv;
                     if (w == 0) {
-                        const unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        unsigned ro = (unsigned)((g0 + kPG * r) * a.ld);
+                        if (ROT) {
+                            const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                            ro = (unsigned)(vm.x * a.ld + vm.y);
+                        }
                         __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bi, mk_rsrc(a.labels),
                                                               ro * 2u, (unsigned)t * 2u, 0);
                         bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
@@ -431,22 +449,48 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
             }
         }
         if (w == 0 && tid == 0) {
-            if (g == 0) p_progress(a.progress, a.prog_base, t);
+            // (rotated: the launch's share of the call, steps scaled to S per launch)
+            if (g == 0) p_progress(a.progress, a.prog_base, ROT ? (int)((long long)t * a.S / t1g) : t, t);
             if (p_abort(a.ctl, a.progress, t)) lds[L_FAIL] = 1.f;  // seen at the next step's check
         }
         __syncthreads();
     }
     if (a.stamps && g == 0 && w == 0 && tid == 0) a.stamps[1] = p_now();
-    if (a.t1 < a.S && w == 0) {
+    if ((ROT || a.t1 < a.S) && w == 0) {
 #pragma unroll
         for (int i = 0; i < NRH; ++i) {
             const int r = 2 * i + hs;
             if (r < NR) {
-                float* st = a.st + (size_t)(g0 + kPG * r) * SW;
+                float* st = a.st + (size_t)vmap_g(r).x * SW;
                 st[j] = lds[L_XA + r * GH + j];
                 st[GH + j] = lds[L_H1 + r * GH + j];
             }
         }
+    }
+}
+
+template <int NR, int MODE, bool ROT, bool DBG>
+__global__ __launch_bounds__(kPT, 1) void k_persist_gen(PersistGenArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_group, s_slot, s_ok;
+    // ---- group formation (as kernels_persist.hip) -------------------------------------------
+    if (threadIdx.x == 0) {
+        int gg, ss;
+        s_ok = p_register(a.ctl, gg, ss);
+        s_group = gg;
+        s_slot = ss;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int g = __builtin_amdgcn_readfirstlane(s_group);
+    const int w = __builtin_amdgcn_readfirstlane(s_slot);
+    if constexpr (ROT && NR >= 2) {  // each group runs its own row count's body
+        if (__builtin_amdgcn_readfirstlane(a.gnr[g]) == NR)
+            gen_body<NR, MODE, true, DBG>(a, lds, g, w);
+        else
+            gen_body<NR - 1, MODE, true, DBG>(a, lds, g, w);
+    } else {
+        gen_body<NR, MODE, false, DBG>(a, lds, g, w);
     }
 }
 
@@ -477,14 +521,31 @@ size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
 // raise the register allocation of the RAW / MOL variants
 template <int NR, int MODE>
 hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
-    if (a.dbg.out) return persist_launch<k_persist_gen<NR, MODE, true>>(persist_gen_lds_bytes(), a, s);
-    return persist_launch<k_persist_gen<NR, MODE, false>>(persist_gen_lds_bytes(), a, s);
+    if constexpr (MODE == 0 && NR >= 2) {
+        if (a.vmap) {  // rotated (RAW, 2-4 rows per group)
+            if (a.dbg.out) return persist_launch<k_persist_gen<NR, MODE, true, true>>(persist_gen_lds_bytes(), a, s);
+            return persist_launch<k_persist_gen<NR, MODE, true, false>>(persist_gen_lds_bytes(), a, s);
+        }
+    }
+    if (a.vmap) return hipErrorInvalidValue;
+    if (a.dbg.out) return persist_launch<k_persist_gen<NR, MODE, false, true>>(persist_gen_lds_bytes(), a, s);
+    return persist_launch<k_persist_gen<NR, MODE, false, false>>(persist_gen_lds_bytes(), a, s);
 }
 
 template <int NR, int MODE>
 int persist_gen_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, MODE, false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist_gen<NR, MODE, false, false>) != hipSuccess) return -1;
+    return (int)fa.localSizeBytes;
+}
+
+// scratch bytes of the rotated RAW instance of nr (2-4) rows per group; -1 if none
+int persist_gen_rot_scratch(int nr) {
+    hipFuncAttributes fa;
+    const void* f = nr == 2 ? (const void*)k_persist_gen<2, 0, true, false>
+                  : nr == 3 ? (const void*)k_persist_gen<3, 0, true, false>
+                  : nr == 4 ? (const void*)k_persist_gen<4, 0, true, false> : nullptr;
+    if (!f || hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 

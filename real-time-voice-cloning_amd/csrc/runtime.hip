@@ -2277,6 +2277,10 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
             ag.t1 = a.t1;
             ag.nr = a.nr;
             ag.rb = a.rb;
+            ag.rows = a.rows;  // (a rotated launch: its own table, and the row map)
+            ag.vmap = a.vmap;
+            ag.gnr = a.gnr;
+            ag.giters = a.giters;
             ag.stamps = a.stamps;
             ag.prog_base = a.prog_base;
             le = launch_persist_gen(ag, st);
@@ -2692,7 +2696,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
                         h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
                         (double)S * B * h->n_classes * 4.0 < 4.0e9;
-    if (fat_rot || rr_rot) {
+    // geneing (k_persist_gen, categorical 'BITS'): as runtimeracer
+    const bool gen_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.gen &&
+                         h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
+                         (double)S * B * h->n_classes * 4.0 < 4.0e9;
+    if (fat_rot || rr_rot || gen_rot) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
         // per-step rates of the rotated instance's two bodies: the (q + 1)-row one at the
@@ -2711,11 +2719,19 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             t_hi = us[nr];
             t_lo = us[nr - 1];
         }
+        if (gen_rot) {  // geneing 10-bit: 3 rows 3.12 us measured (single launch, C2 shape); the
+            // 2-row rate the best of a scan of splits (C2 3.13 -> 3.01 us per step,
+            // profiles/r05/gen_rotation/); 1 / 4 rows scaled from the round-2 points (estimates)
+            static const double gr[kPNR + 1] = {0, 1.98, 2.47, 3.12, 3.64};
+            t_hi = gr[nr];
+            t_lo = gr[nr - 1];
+        }
         if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
-        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr) : persist_rot_scratch(nr, h->cfg.mode);
+        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr)
+                     : gen_rot ? persist_gen_rot_scratch(nr) : persist_rot_scratch(nr, h->cfg.mode);
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
             plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
             h->p_plan.clear();

@@ -28,7 +28,11 @@ def _run(model_type, mode, bits, n_utts, frames=1000, target=11000, overlap=550)
     return m.plan_info()
 
 
-def test_c2_shape_geneing_is_one_launch_of_3_rows_per_group():
+def test_c2_shape_geneing_is_rotated_over_three_launches(monkeypatch):
+    """geneing 10-bit at C2 (18 rows): the rotated k_persist_gen, three launches
+    of 3 / 2 rows per group; WRNN_PERSIST_ROT=0 restores the single 3-row launch."""
+    assert _run('geneing-wavernn', 'BITS', 10, 1) == [(0, 3, False)] * 3
+    monkeypatch.setenv('WRNN_PERSIST_ROT', '0')
     assert _run('geneing-wavernn', 'BITS', 10, 1) == [(0, 3, False)]
 
 

@@ -220,14 +220,17 @@ def test_rotated_ragged_utterances_equal_single_launch(monkeypatch):
     assert len(d) == 0, f'first difference {d[np.argmin(d[:, 1])].tolist()}'
 
 
-@pytest.mark.parametrize('bits,rows', [(9, 18), (10, 20), (9, 17)])
-def test_rotated_runtimeracer_labels_equal_single_launch(bits, rows, monkeypatch):
-    """The runtimeracer register-resident kernel rotated (k_persist_rr<..., ROT>: rows at their
-    own step offsets, the four GRUs' chunk state across launches, P1 and the noise streams read
-    at each row's own step): labels, and the logits recorded around the launch boundaries, equal
-    the single launch's bit for bit."""
+@pytest.mark.parametrize('model_type,mode,bits,rows', [
+    ('runtimeracer-wavernn', 'RAW', 9, 18), ('runtimeracer-wavernn', 'RAW', 10, 20),
+    ('runtimeracer-wavernn', 'RAW', 9, 17),
+    ('geneing-wavernn', 'BITS', 10, 18), ('geneing-wavernn', 'BITS', 9, 20), ('geneing-wavernn', 'BITS', 10, 17)])
+def test_rotated_runtimeracer_geneing_labels_equal_single_launch(model_type, mode, bits, rows, monkeypatch):
+    """The runtimeracer / geneing register-resident kernels rotated (k_persist_rr / k_persist_gen
+    <..., ROT>: rows at their own step offsets, the GRUs' chunk state across launches, P1 and the
+    noise streams read at each row's own step): labels, and the logits recorded around the launch
+    boundaries, equal the single launch's bit for bit."""
     from wavernn_amd.synth import synth_mel
-    m, hp = _model(bits=bits, model_type='runtimeracer-wavernn')
+    m, hp = _model(mode=mode, bits=bits, model_type=model_type)
     mel = synth_mel(_frames_for(m, rows), 600 + rows)
     _, (K, nh, nl), _ = _call(m, mel, monkeypatch, rot=True)
     steps = [0, nh - 1, nh, nl, nh + nl - 1, nh + nl, 2 * nl, 4799]

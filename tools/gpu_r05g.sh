@@ -1,19 +1,10 @@
-# round 5: time-sliced wide launches -- rotation / plan / full-size / wide tests, C4 bench, C2 bench
-set -o pipefail
-OUT=${OUT:-gpurun_out/r05g}
-mkdir -p $OUT
-timeout -k 10 800 python -u -m pytest tests/test_gpu_rotation.py tests/test_gpu_plan.py tests/test_gpu_fullsize.py tests/test_gpu_wide.py tests/test_gpu_logits.py -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1
-rc=$?
-grep -E "passed|failed" $OUT/tests.log | tail -2; grep -E "^FAILED" $OUT/tests.log | head
-echo "tests rc=$rc"
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-for args in "--utts-per-gpu 8 --steps 3 --warmup 1 --cpu-seconds 0" "--steps 5 --warmup 1 --cpu-seconds 0"; do
-  timeout -k 10 300 python -u bench.py $args > $OUT/bench_$(echo $args | cut -c3-7).log 2>&1 || { echo "bench fail $args"; exit 1; }
-  python - $OUT/bench_$(echo $args | cut -c3-7).log <<'PY'
-import json,sys
-for l in open(sys.argv[1]):
-    if l.startswith('{'):
-        d=json.loads(l); r=d['roofline']; print(d['config']['workload'][:30], 'value', round(d['value']), 'ms/step', round(d['ms_per_step'],2), 'us/step', round(r['us_per_step'],3), 'call_us/step', round(r.get('call_us_per_step',0),3), 'steps/launch', r.get('steps_per_launch'), 'parity', d.get('parity',{}).get('labels_equal'))
-PY
+set -u
+mkdir -p gpurun_out/genrot
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -v -rA --timeout 240 --timeout-method thread tests/test_gpu_rotation.py -k "runtimeracer_geneing" tests/test_gpu_plan.py > gpurun_out/genrot/tests.log 2>&1 || { tail -30 gpurun_out/genrot/tests.log; exit 1; }
+tail -3 gpurun_out/genrot/tests.log
+for rot in 0 1; do
+  WRNN_PERSIST_ROT=$rot timeout -k 10 120 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model geneing-wavernn --mode BITS --bits 10 > gpurun_out/genrot/rot$rot.log 2>&1 || exit 1
+  grep '^{' gpurun_out/genrot/rot$rot.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('rot', $rot, d['value'], d['roofline'].get('us_per_step'), d['ms_per_step'])"
 done
-exit $rc
+RATES="3.91,3.26 3.91,3.1 3.91,3.4 3.91,2.95" BENCH_ARGS="--model geneing-wavernn --mode BITS --bits 10" TAGS=.gen bash tools/rot_tune.sh
