@@ -88,7 +88,7 @@ __device__ __forceinline__ bool poll_rows(rsrc_t xr, unsigned so, unsigned seq, 
 //      and the noise are read at the row's own step, labels / logits written there.
 template <int NR, int MODE, bool ROT, bool DBG>
 __device__ __forceinline__ void gen_body(const PersistGenArgs& a, float* lds, const int g, const int w) {
-    static_assert(!(ROT && MODE != 0), "rotated geneing launches are RAW");
+    static_assert(!(ROT && MODE == 2), "rotated geneing launches are BITS or MOL");
     const int tid = threadIdx.x;
     const int g0 = a.rb + g;
     const int t1g = ROT ? __builtin_amdgcn_readfirstlane(a.giters[g]) : a.t1;
@@ -167,9 +167,14 @@ __device__ __forceinline__ void gen_body(const PersistGenArgs& a, float* lds, co
             }
         }
         // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
-        if (MODE == 1 && tid < 32 * NR && (tid & 31) < 11)
-            pgum = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + g0 + kPG * (tid >> 5)) * kMolNoise),
-                       (unsigned)(tid & 31) * 4u, 0);
+        if (MODE == 1 && tid < 32 * NR && (tid & 31) < 11) {
+            size_t ro = (size_t)t * a.B + g0 + kPG * (tid >> 5);
+            if constexpr (ROT) {  // (the row's own step)
+                const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[tid >> 5];
+                ro = (size_t)(t + vm.y) * a.B + vm.x;
+            }
+            pgum = bld(mk_rsrc(a.gumbel + ro * kMolNoise), (unsigned)(tid & 31) * 4u, 0);
+        }
         float pP[NRH][3], pC[NRH];
         {  // (unconditional, step clamped: every path to the back edge consumes these loads)
             const int tn = nxt ? t + 1 : t;
@@ -426,7 +431,14 @@ __device__ __forceinline__ void gen_body(const PersistGenArgs& a, float* lds, co
             }
             if (k == 0) {
                 lds[L_SX + r] = xv;
-                if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+                if (w == 0) {
+                    unsigned ro = (unsigned)(row * a.ld);
+                    if (ROT) {
+                        const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                        ro = (unsigned)(vm.x * a.ld + vm.y);
+                    }
+                    bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                }
             }
         }
         __syncthreads();
@@ -521,8 +533,8 @@ size_t persist_gen_xbuf_floats() { return (size_t)kPG * QX_GROUP; }
 // raise the register allocation of the RAW / MOL variants
 template <int NR, int MODE>
 hipError_t launch_persist_gen_t(const PersistGenArgs& a, hipStream_t s) {
-    if constexpr (MODE == 0 && NR >= 2) {
-        if (a.vmap) {  // rotated (RAW, 2-4 rows per group)
+    if constexpr (MODE != 2 && NR >= 2) {
+        if (a.vmap) {  // rotated (BITS / MOL, 2-4 rows per group)
             if (a.dbg.out) return persist_launch<k_persist_gen<NR, MODE, true, true>>(persist_gen_lds_bytes(), a, s);
             return persist_launch<k_persist_gen<NR, MODE, true, false>>(persist_gen_lds_bytes(), a, s);
         }
@@ -539,12 +551,18 @@ int persist_gen_spill_t() {
     return (int)fa.localSizeBytes;
 }
 
-// scratch bytes of the rotated RAW instance of nr (2-4) rows per group; -1 if none
-int persist_gen_rot_scratch(int nr) {
+// scratch bytes of the rotated BITS (mode 0) / MOL (1) instance of nr (2-4) rows per group; -1 if none
+int persist_gen_rot_scratch(int nr, int mode) {
     hipFuncAttributes fa;
-    const void* f = nr == 2 ? (const void*)k_persist_gen<2, 0, true, false>
-                  : nr == 3 ? (const void*)k_persist_gen<3, 0, true, false>
-                  : nr == 4 ? (const void*)k_persist_gen<4, 0, true, false> : nullptr;
+    const void* f = nullptr;
+    if (mode == 0)
+        f = nr == 2 ? (const void*)k_persist_gen<2, 0, true, false>
+          : nr == 3 ? (const void*)k_persist_gen<3, 0, true, false>
+          : nr == 4 ? (const void*)k_persist_gen<4, 0, true, false> : nullptr;
+    else if (mode == 1)
+        f = nr == 2 ? (const void*)k_persist_gen<2, 1, true, false>
+          : nr == 3 ? (const void*)k_persist_gen<3, 1, true, false>
+          : nr == 4 ? (const void*)k_persist_gen<4, 1, true, false> : nullptr;
     if (!f || hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }

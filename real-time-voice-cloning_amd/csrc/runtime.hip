@@ -2696,10 +2696,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
                         h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
                         (double)S * B * h->n_classes * 4.0 < 4.0e9;
-    // geneing (k_persist_gen, categorical 'BITS'): as runtimeracer
+    // geneing (k_persist_gen, categorical 'BITS' and MOL): as runtimeracer
     const bool gen_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.gen &&
-                         h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
-                         (double)S * B * h->n_classes * 4.0 < 4.0e9;
+                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) &&
+                         h->p_plan[0].nr >= 2 && (double)S * B * h->n_classes * 4.0 < 4.0e9;
     if (fat_rot || rr_rot || gen_rot) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
@@ -2723,15 +2723,19 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             // 2-row rate the best of a scan of splits (C2 3.13 -> 3.01 us per step,
             // profiles/r05/gen_rotation/); 1 / 4 rows scaled from the round-2 points (estimates)
             static const double gr[kPNR + 1] = {0, 1.98, 2.47, 3.12, 3.64};
-            t_hi = gr[nr];
-            t_lo = gr[nr - 1];
+            // MOL: 3 rows 2.60 us measured; 2 rows the best of its own split scan (2.06-2.25:
+            // C2 shape 2.62 -> 2.43 us per step at 2.15)
+            static const double gm[kPNR + 1] = {0, 1.72, 2.15, 2.60, 3.03};
+            const double* us = h->cfg.mode == WRNN_MODE_MOL ? gm : gr;
+            t_hi = us[nr];
+            t_lo = us[nr - 1];
         }
         if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
         const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr)
-                     : gen_rot ? persist_gen_rot_scratch(nr) : persist_rot_scratch(nr, h->cfg.mode);
+                     : gen_rot ? persist_gen_rot_scratch(nr, h->cfg.mode) : persist_rot_scratch(nr, h->cfg.mode);
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
             plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
             h->p_plan.clear();

@@ -378,7 +378,7 @@ struct PersistGenArgs {
     uint32_t k0, k1;        // Philox key (BETA draws in-kernel)
     int prog_base;
     DbgLogits dbg;
-    // rotated launch (RAW; null otherwise): virtual row v = g + 8 r ->
+    // rotated launch (BITS / MOL; null otherwise): virtual row v = g + 8 r ->
     // (physical row, step offset), `rows` the launch's RowInfo table by virtual row, rows and
     // steps per group
     const int2* vmap;
@@ -387,7 +387,7 @@ struct PersistGenArgs {
 };
 
 hipError_t launch_persist_gen(const PersistGenArgs& a, hipStream_t s);
-int persist_gen_rot_scratch(int nr);  // the rotated RAW instance's scratch bytes (-1: none)
+int persist_gen_rot_scratch(int nr, int mode);  // the rotated BITS / MOL instance's scratch bytes (-1: none)
 hipError_t launch_persist_gen_init(const PersistGenArgs& a, hipStream_t s);
 int persist_gen_variant_ok(int nr, int cpw, int mode);
 size_t persist_gen_lds_bytes();

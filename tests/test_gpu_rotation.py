@@ -67,14 +67,24 @@ def test_rotated_labels_equal_single_launch(rows, monkeypatch):
     assert len(d) == 0, f'{rows} rows: first difference {d[np.argmin(d[:, 1])].tolist()}'
 
 
-def test_rotated_mol_samples_equal_single_launch(monkeypatch):
+@pytest.mark.parametrize('model_type,rows', [('fatchord-wavernn', 18), ('geneing-wavernn', 18),
+                                             ('geneing-wavernn', 20)])
+def test_rotated_mol_samples_equal_single_launch(model_type, rows, monkeypatch):
+    """MOL rotated (k_persist / k_persist_gen <..., MOL, ROT>: the 11 noise draws and the sample
+    column at each row's own step): samples, and the logits around the launch boundaries, equal
+    the single launch's bit for bit."""
     from wavernn_amd.synth import synth_mel
-    m, hp = _model('MOL')
-    mel = synth_mel(_frames_for(m, 18), 77)
-    a, ra, _ = _call(m, mel, monkeypatch, rot=True)
-    b, rb, _ = _call(m, mel, monkeypatch, rot=False)
-    assert ra[0] > 1 and rb[0] == 0
+    m, hp = _model('MOL', model_type=model_type)
+    mel = synth_mel(_frames_for(m, rows), 77)
+    _, (K, nh, nl), _ = _call(m, mel, monkeypatch, rot=True)
+    steps = [0, nh - 1, nh, nl, nh + nl - 1, nh + nl, 2 * nl, 4799]
+    a, ra, la = _call(m, mel, monkeypatch, rot=True, debug_steps=steps)
+    b, rb, lb = _call(m, mel, monkeypatch, rot=False, debug_steps=steps)
+    assert a.shape[0] == rows and ra[0] > 1 and rb[0] == 0, (a.shape, ra, rb)
     assert np.array_equal(a, b)
+    for s in steps:
+        assert np.isfinite(la[s]).all(), s
+        assert np.array_equal(la[s], lb[s]), s
 
 
 def test_rotated_logit_capture_equals_single_launch(monkeypatch):
