@@ -186,7 +186,6 @@ __device__ __forceinline__ bool poll_hop_hx(rsrc_t xr, unsigned so, unsigned seq
 //      and the noise are read at the row's own step, labels / logits written there.
 template <int NR, bool MOL, bool ROT, bool DBG>
 __device__ __forceinline__ void rr_body(const PersistRRArgs& a, float* lds, const int g, const int w) {
-    static_assert(!(ROT && MOL), "rotated runtimeracer launches are RAW");
     const int tid = threadIdx.x;
     const int g0 = a.rb + g;                  // first (virtual) fold row of this group in this launch
     const int t1g = ROT ? __builtin_amdgcn_readfirstlane(a.giters[g]) : a.t1;
@@ -481,9 +480,14 @@ __device__ __forceinline__ void rr_body(const PersistRRArgs& a, float* lds, cons
                            (unsigned)(lrow * a.n_classes + cls) * 4u, 0);
         }
         // MOL: sampling lane (row tid / 32, k = tid % 32 < 11) holds draw k of its row
-        if (MOL && tid < 32 * NR && (tid & 31) < 11)
-            pgum = bld(mk_rsrc(a.gumbel + ((size_t)t * a.B + g0 + kPG * (tid >> 5)) * kMolNoise),
-                       (unsigned)(tid & 31) * 4u, 0);
+        if (MOL && tid < 32 * NR && (tid & 31) < 11) {
+            size_t ro = (size_t)t * a.B + g0 + kPG * (tid >> 5);
+            if constexpr (ROT) {  // (the row's own step)
+                const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[tid >> 5];
+                ro = (size_t)(t + vm.y) * a.B + vm.x;
+            }
+            pgum = bld(mk_rsrc(a.gumbel + ro * kMolNoise), (unsigned)(tid & 31) * 4u, 0);
+        }
         // ================= stage 4: q3 fc1 ==================================================
         if (q == 3) {
             __builtin_amdgcn_s_setprio(2);
@@ -703,7 +707,14 @@ __device__ __forceinline__ void rr_body(const PersistRRArgs& a, float* lds, cons
                     xv = xv > 1.f ? 1.f : xv;
                 }
                 lds[L_SX + r] = xv;
-                if (w == 0) bst(xv, mk_rsrc(a.samples), (unsigned)(row * a.ld) * 4u, (unsigned)t * 4u);
+                if (w == 0) {
+                    unsigned ro = (unsigned)(row * a.ld);
+                    if (ROT) {
+                        const int2 vm = reinterpret_cast<const int2*>(lds + L_VM)[r];
+                        ro = (unsigned)(vm.x * a.ld + vm.y);
+                    }
+                    bst(xv, mk_rsrc(a.samples), ro * 4u, (unsigned)t * 4u);
+                }
             }
         }
         __syncthreads();
@@ -822,8 +833,8 @@ size_t persist_rr_xbuf_floats() { return (size_t)kPG * RX_GROUP; }
 
 template <int NR, bool MOL>
 hipError_t launch_persist_rr_t(const PersistRRArgs& a, hipStream_t s) {
-    if constexpr (!MOL && NR >= 2) {
-        if (a.vmap) {  // rotated (RAW, 2-4 rows per group)
+    if constexpr (NR >= 2) {
+        if (a.vmap) {  // rotated (RAW / MOL, 2-4 rows per group)
             if (a.dbg.out) return persist_launch<k_persist_rr<NR, MOL, true, true>>(persist_rr_lds_bytes(), a, s);
             return persist_launch<k_persist_rr<NR, MOL, true, false>>(persist_rr_lds_bytes(), a, s);
         }
@@ -839,12 +850,18 @@ int persist_rr_spill_t() {
     if (hipFuncGetAttributes(&fa, (const void*)k_persist_rr<NR, MOL, false, false>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
-// scratch bytes of the rotated RAW instance of nr (2-4) rows per group; -1 if none
-int persist_rr_rot_scratch(int nr) {
+// scratch bytes of the rotated RAW / MOL instance of nr (2-4) rows per group; -1 if none
+int persist_rr_rot_scratch(int nr, bool mol) {
     hipFuncAttributes fa;
-    const void* f = nr == 2 ? (const void*)k_persist_rr<2, false, true, false>
-                  : nr == 3 ? (const void*)k_persist_rr<3, false, true, false>
-                  : nr == 4 ? (const void*)k_persist_rr<4, false, true, false> : nullptr;
+    const void* f = nullptr;
+    if (!mol)
+        f = nr == 2 ? (const void*)k_persist_rr<2, false, true, false>
+          : nr == 3 ? (const void*)k_persist_rr<3, false, true, false>
+          : nr == 4 ? (const void*)k_persist_rr<4, false, true, false> : nullptr;
+    else
+        f = nr == 2 ? (const void*)k_persist_rr<2, true, true, false>
+          : nr == 3 ? (const void*)k_persist_rr<3, true, true, false>
+          : nr == 4 ? (const void*)k_persist_rr<4, true, true, false> : nullptr;
     if (!f || hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }

@@ -2691,10 +2691,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     const bool fat_rot = use_p && h->p1_ring && h->p_plan.size() == 1 && !h->p_plan[0].wide && !h->pw.rr &&
                          !h->pw.gen && h->pw.cpw <= 16 &&
                          (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
-    // runtimeracer (k_persist_rr, RAW): P1 and the noise from their streams at each row's own
+    // runtimeracer (k_persist_rr, RAW / MOL): P1 and the noise from their streams at each row's own
     // step (the noise stream addressed with 32-bit offsets: < 4 GiB)
     const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
-                        h->cfg.mode == WRNN_MODE_RAW && h->p_plan[0].nr >= 2 &&
+                        (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2 &&
                         (double)S * B * h->n_classes * 4.0 < 4.0e9;
     // geneing (k_persist_gen, categorical 'BITS' and MOL): as runtimeracer
     const bool gen_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.gen &&
@@ -2715,7 +2715,10 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         if (rr_rot) {  // runtimeracer, measured single-launch step times at 1-4 rows per group
             static const double rr9[kPNR + 1] = {0, 6.3, 7.0, 7.78, 8.8};   // 9-bit (2 / 4 rows: estimates)
             static const double rr10[kPNR + 1] = {0, 6.5, 7.26, 8.14, 9.23};  // 10-bit (profiles/r05/rr_rates/)
-            const double* us = h->pw.cpw > 16 ? rr10 : rr9;
+            // MOL: 3 rows 7.42 us measured; 2 rows the best of its own split scan (6.0-6.9: C2
+            // shape 7.50 -> 7.03 us per step at 6.6, profiles/r05/rr_rotation/mol/)
+            static const double rrm[kPNR + 1] = {0, 5.9, 6.6, 7.42, 8.4};
+            const double* us = h->cfg.mode == WRNN_MODE_MOL ? rrm : h->pw.cpw > 16 ? rr10 : rr9;
             t_hi = us[nr];
             t_lo = us[nr - 1];
         }
@@ -2734,7 +2737,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
-        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr)
+        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr, h->cfg.mode == WRNN_MODE_MOL)
                      : gen_rot ? persist_gen_rot_scratch(nr, h->cfg.mode) : persist_rot_scratch(nr, h->cfg.mode);
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
             plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {

@@ -331,7 +331,7 @@ struct PersistRRArgs {
 };
 
 hipError_t launch_persist_rr(const PersistRRArgs& a, hipStream_t s);
-int persist_rr_rot_scratch(int nr);  // the rotated RAW instance's scratch bytes (-1: none)
+int persist_rr_rot_scratch(int nr, bool mol);  // the rotated RAW / MOL instance's scratch bytes (-1: none)
 // Wide-row runtimeracer launch (kernels_persist_wide_rr.hip): up to kPWideRows rows per XCD
 // group, the group split into two halves of 16 slots that own 16 units of alternate layers,
 // fp32 MFMA products, RAW categorical with 512 or 1024 classes (cpw = n / 16 per B slot).

@@ -68,9 +68,10 @@ def test_rotated_labels_equal_single_launch(rows, monkeypatch):
 
 
 @pytest.mark.parametrize('model_type,rows', [('fatchord-wavernn', 18), ('geneing-wavernn', 18),
-                                             ('geneing-wavernn', 20)])
+                                             ('geneing-wavernn', 20), ('runtimeracer-wavernn', 18),
+                                             ('runtimeracer-wavernn', 17)])
 def test_rotated_mol_samples_equal_single_launch(model_type, rows, monkeypatch):
-    """MOL rotated (k_persist / k_persist_gen <..., MOL, ROT>: the 11 noise draws and the sample
+    """MOL rotated (k_persist / k_persist_gen / k_persist_rr <..., MOL, ROT>: the 11 noise draws and the sample
     column at each row's own step): samples, and the logits around the launch boundaries, equal
     the single launch's bit for bit."""
     from wavernn_amd.synth import synth_mel

@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-LINES = ('bench', 'c4', 'rr', 'b10', 'gen', 'gen_norot')
+LINES = ('bench', 'c4', 'rr', 'b10', 'c3', 'gen', 'gen_norot', 'gen_mol', 'rr_mol', 'rr9')
 
 
 def bench_line(path):

@@ -8,7 +8,8 @@
 #   bench    : default line (C2, CPU baseline, parity, logit gate), counters from the pass above
 #   c4       : --utts-per-gpu 8                  rr    : runtimeracer 10-bit defaults, 8 utts
 #   b10      : fatchord 10-bit defaults (3000 / 1500), 8 utts (the 1024-class wide slices)
-#   gen      : geneing 10-bit C2 shape (the rotated k_persist_gen), rotation off and on
+#   gen      : geneing 10-bit C2 shape (the rotated k_persist_gen), rotation off and on; the other
+#              rotated C2-shape lines: geneing MOL, runtimeracer MOL and 9-bit, fatchord MOL (C3)
 # (three gpurun calls: STEPS=tests,smoke | pmc,bench,c4,rr,b10 | rehearse,phase,prof -- with
 #  WRNN_PMC_TRAFFIC pointing the later benches at the pass's pmc_traffic.json)
 #   rehearse : the N>1 path with 2 ranks on one GPU (gloo), CPU baseline + parity on rank 0
@@ -58,6 +59,10 @@ fi
 if [[ ,$S, == *,gen,* ]]; then
   run gen 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model geneing-wavernn --mode BITS --bits 10
   run gen_norot 300 env WRNN_PERSIST_ROT=0 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model geneing-wavernn --mode BITS --bits 10
+  run gen_mol 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model geneing-wavernn --mode MOL
+  run rr_mol 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --mode MOL
+  run rr9 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --model runtimeracer-wavernn --bits 9
+  run c3 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --mode MOL
 fi
 [[ ,$S, == *,rehearse,* ]] && run rehearse 400 env WRNN_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --cpu-seconds 10
 [[ ,$S, == *,phase,* ]] && run phase 200 env WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0
