@@ -2695,11 +2695,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // step (the noise stream addressed with 32-bit offsets: < 4 GiB)
     const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2 &&
-                        (double)S * B * h->n_classes * 4.0 < 4.0e9;
+                        (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
     // geneing (k_persist_gen, categorical 'BITS' and MOL): as runtimeracer
     const bool gen_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.gen &&
                          (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) &&
-                         h->p_plan[0].nr >= 2 && (double)S * B * h->n_classes * 4.0 < 4.0e9;
+                         h->p_plan[0].nr >= 2 && (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
     if (fat_rot || rr_rot || gen_rot) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;
