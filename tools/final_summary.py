@@ -40,6 +40,8 @@ def main():
             c2 = d
         wl = d['config']['workload'] + (' (rotation off)' if name == 'gen_norot' else '')
         tr = f"{r['traffic'] / 1e9:.3f}" if r.get('traffic') else 'n/a'
+        if name.endswith('_norot'):  # (the counters are filed by workload: the rotated plan's launch)
+            tr = 'n/a'
         mb = f"{r['mfma_busy_frac']:.2f}" if 'mfma_busy_frac' in r else 'n/a'
         L.append(f"| {name} | {wl} | {d['value']:,.0f} | {d['ms_per_step']:.2f} | {r['kernel']} | "
                  f"{r['us_per_step']:.3f} | {r['call_us_per_step']:.3f} | {r['launches_per_generate']} | {tr} | {mb} | "

@@ -40,8 +40,9 @@ if [[ ,$S, == *,pmc,* ]]; then
   python -c "import sys; sys.path[:0]=['.', 'real-time-voice-cloning_amd']; import bench; print(bench.lib_build_id())" > $P/lib_build
   B="/usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 --no-timing"
   SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-  for m in c2 c4 rr b10; do
+  for m in ${PMC_SET:-c2 c4 rr b10 gen}; do
     A=""; K="k_persist<"
+    [ $m = gen ] && A="--model geneing-wavernn --mode BITS --bits 10" && K="k_persist_gen<"
     [ $m = c4 ] && A="--utts-per-gpu 8" && K="k_persist_wide<"
     [ $m = rr ] && A="$RR" && K="k_persist_wide_rr"
     [ $m = b10 ] && A="$B10" && K="k_persist_wide<"

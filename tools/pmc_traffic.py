@@ -48,6 +48,8 @@ WORKLOADS = {
     'rr': (' --model runtimeracer-wavernn --bits 10 --target 6000 --overlap 1000 --utts-per-gpu 8',
            workload('runtimeracer-wavernn', 'RAW 10-bit mu-law', utts=8, target=6000, overlap=1000),
            'k_persist_wide_rr'),
+    'gen': (' --model geneing-wavernn --mode BITS --bits 10',
+            workload('geneing-wavernn', 'BITS 10-bit'), 'k_persist_gen'),
 }
 
 
