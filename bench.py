@@ -343,6 +343,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_rank = dt
     if world > 1:
         t = torch.tensor([dt], device='cpu' if rehearse else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -357,6 +358,7 @@ def main():
              else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else ''))
     workload = workload_of(U, args.frames, args.model, wname, args.target, args.overlap)
     roof = None
+    us_rank = None
     info = model.stage_info() if not args.no_timing else []
     rows_per_gpu = U * model.fold_shape(args.frames, True, args.target, args.overlap)[0]
     if info:
@@ -429,6 +431,25 @@ def main():
                       'active_frac', 'sq_source'):
                 if k in pmc:
                     roof[k] = pmc[k]
+    ranks = None
+    if world > 1:
+        # every rank's identity and timing (all-gathered), so an N > 1 line proves N distinct
+        # GPUs and shows the slowest rank: world size as the process group sees it, hostname,
+        # PCI address and UUID of the rank's device, its dominant kernel's average launch time
+        # and its own wall time of the timed region
+        import socket
+        pr = torch.cuda.get_device_properties(dev)
+        me = {'rank': rank, 'local_rank': local, 'hostname': socket.gethostname(),
+              'pci': f'{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}',
+              'uuid': str(getattr(pr, 'uuid', '')), 'kernel_avg_us': us_rank, 'wall_s': dt_rank}
+        per = [None] * world
+        dist.all_gather_object(per, me)
+        timed = [r for r in per if r['kernel_avg_us'] is not None]
+        ranks = {'world_size_pg': dist.get_world_size(), 'per_rank': per,
+                 'distinct_devices': len({(r['hostname'], r['pci'], r['uuid']) for r in per}),
+                 'slowest_rank_kernel': (max(timed, key=lambda r: r['kernel_avg_us'])['rank']
+                                         if timed else None),
+                 'slowest_rank_wall': max(per, key=lambda r: r['wall_s'])['rank']}
     fb = model.fallback_info()
     result = {
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',
@@ -449,6 +470,8 @@ def main():
         'roofline': roof,
         'cpu_baseline': None,
     }
+    if ranks is not None:
+        result['ranks'] = ranks
     if fb[0]:
         result['config']['fallback_reason'] = fb[1]
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -24,8 +24,8 @@
 // -> gh2 of the next step (kept local) in hops B and C. Redundantly in every workgroup: the
 // sample of step t and GRU1 of step t+1 for all 512 units (so x1/h1 never need an exchange).
 // Sampling: argmax_k (l_k + G_k), G_k = -log q_k with q the RNG contract's Exp(1) variate,
-// G in fixed point to 2^-27 and the sum in float64 (persist_common.h cand_key) -- the
-// reference's argmax((softmax(l)/sum)/q) without the fp32 rounding of round 4's l + g.
+// G in fixed point to 2^-27 and l + G formed exactly as an fp32 pair (TwoSum, cand_key.h) --
+// the reference's argmax((softmax(l)/sum)/q) without the fp32 rounding of round 4's l + g.
 // Every spin is bounded; on a timeout the kernel sets an error code and every group exits.
 #include "wrnn_kernels.h"
 #include "persist_common.h"
@@ -38,11 +38,6 @@
 // is everything in one object (tools/build_variant.sh).
 #ifndef WRNN_PERSIST_PART
 #define WRNN_PERSIST_PART 0
-#endif
-// where the RAW candidate keys are formed: 1 = by the fc3 epilogue lanes, 0 = by wave 0 as it
-// reduces the slot's candidates (A/B)
-#ifndef WRNN_KEY_EPI
-#define WRNN_KEY_EPI 0
 #endif
 
 namespace wrnn {
@@ -86,6 +81,51 @@ static_assert(L_W % 4 == 0, "weights must be 16-byte aligned");
 static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 KiB");
 
 
+// ---- sparse products (SP instances: pruned checkpoints) --------------------
+// The slot's weights as its live 1 x 4 blocks (the Pruner's groups, vocoder/pruner.py:60-88) in
+// LDS (runtime.hip pack_persist_sparse): per product set and 16-lane row group (one output row
+// of the slot), entry e of lane kc at float4 index base + 16 e, the lane's base and masks in its
+// four words of PersistArgs::wreg; mask bit 8 j + q says block q of gate j (columns
+// 4 (16 q + kc) .. + 3, the dense kernel's register float4 wr[8 j + q]) is live. Each round takes
+// the next live block of every gate at once; a lane with none left reads the zero row
+// (kPSpZero) against block 0 of X, so its fma adds an exact zero. Every (row, gate) accumulator
+// sees its live blocks in increasing q -- the dense kernel's order minus products that are exact
+// zeros -- so the sums are bit-identical to the dense kernel's on the same weights.
+// RM: the rows (bit r) accumulated.
+template <int NR, int G, int RM = 0xF>
+__device__ __forceinline__ void sp_products(const float4* Wsp, const float4* Xs, unsigned (&m)[G],
+                                            unsigned (&p)[G], const int kc, v2f (&acc)[NR][G]) {
+    const unsigned zb = (unsigned)(kPSpZero + kc);
+    while (true) {
+        unsigned any = 0u;
+#pragma unroll
+        for (int j = 0; j < G; ++j) any |= m[j];
+        if (any == 0u) break;
+        unsigned q[G];
+        float4 wv[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const bool v = m[j] != 0u;
+            q[j] = v ? (unsigned)__builtin_ctz(m[j]) : 0u;
+            m[j] &= m[j] - 1u;
+            wv[j] = Wsp[v ? p[j] : zb];
+            p[j] += v ? 16u : 0u;
+        }
+        // (fully unrolled by the compiler: constant trip counts; an explicit pragma here is
+        // reported as not applied once the row mask has removed rows)
+        for (int r = 0; r < NR; ++r)
+            if ((RM >> r) & 1)
+                for (int j = 0; j < G; ++j) dot4(acc[r][j], wv[j], Xs[r * kPK4 + 16 * q[j] + kc]);
+    }
+}
+// rows r < NR of the W_hh2 window WIN (r % 3 == WIN) as a row mask
+constexpr int hh2_rowmask(int win, int nr) {
+    int m = 0;
+    for (int r = 0; r < nr; ++r)
+        if (r % 3 == win) m |= 1 << r;
+    return m;
+}
+
 // P1R: P1 from the in-launch ring (PersistArgs::p1q) instead of the [S][B][4H] stream.
 // DBG: the instance that records logits for the teacher-forced gate (wrnn_set_debug_steps)
 // ROT: a rotated launch (PersistArgs::vmap): row slot r of the group is the
@@ -94,9 +134,11 @@ static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 Ki
 //      RowInfo table (a.rows, by virtual row) carries rel0 + offset, so every per-frame /
 //      per-position lookup follows; noise, labels, samples, state and logits use the physical
 //      row and the offset step.
-template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG>
+// SP: the sparse instance (pruned weights, block lists in LDS; sp_products above)
+template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG, bool SP>
 __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, const int g, const int w) {
     static_assert(!ROT || P1R, "rotated launches form P1 in the ring");
+    static_assert(!SP || P1R, "sparse instances form P1 in the ring");
     const int tid = threadIdx.x;
     const int g0 = a.rb + g;  // first (virtual) fold row of this group in this launch
     // the group's step range: [t0, t1) (rotated: its own step count, offsets per row)
@@ -127,17 +169,25 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
     }
 
     // ---- weights: registers and LDS -----------------------------------------------------
-    constexpr int NW = FC3R ? 40 : 32;
+    constexpr int NW = SP ? 1 : FC3R ? 40 : 32;
     float4 wr[NW];
+    // SP: the lane's masks and list bases (x: set A | fc << 24, y: W_hh2 | fc3 << 24,
+    // z / w: their bases, 16 bits each) -- the whole slot image goes to LDS
+    uint4 si = make_uint4(0u, 0u, 0u, 0u);
     {
-        const float4* src = a.wreg + ((size_t)w * kPT + tid) * NW;
+        if constexpr (SP) {
+            si = reinterpret_cast<const uint4*>(a.wreg)[(size_t)w * kPT + tid];
+        } else {
+            const float4* src = a.wreg + ((size_t)w * kPT + tid) * NW;
 #pragma unroll
-        for (int i = 0; i < NW; ++i) wr[i] = src[i];
+            for (int i = 0; i < NW; ++i) wr[i] = src[i];
+        }
         const float4* hs = a.wlds + (size_t)w * kPLdsW4;
         float4* hd = reinterpret_cast<float4*>(lds + L_W);
-        const int n4 = FC3R ? 16 * 3 * kPK4 : kPLdsW4;
+        const int n4 = FC3R && !SP ? 16 * 3 * kPK4 : kPLdsW4;
         for (int i = tid; i < n4; i += kPT) hd[i] = hs[i];
     }
+    const float4* Wsp = reinterpret_cast<const float4*>(lds + L_W);
     // ---- chunk state -----------------------------------------------------------------------
     // thread tid = unit j of the redundant GRU1; lanes kc < NR of og < 16 own (u, row kc) of GRU2
     float h1[NR], h2r = 0.f;
@@ -326,6 +376,13 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             for (int r = 0; r < NR; ++r)
 #pragma unroll
                 for (int j = 0; j < 3; ++j) acc[r][j] = (v2f){0.f, 0.f};
+            if constexpr (SP) {
+                const unsigned mx = si.x, pb = si.z & 0xffffu;
+                unsigned m[3] = {mx & 0xffu, (mx >> 8) & 0xffu, (mx >> 16) & 0xffu};
+                const unsigned c0 = (unsigned)__builtin_popcount(m[0]), c1 = (unsigned)__builtin_popcount(m[1]);
+                unsigned p[3] = {pb, pb + 16u * c0, pb + 16u * (c0 + c1)};
+                sp_products<NR, 3>(Wsp, Xs, m, p, kc, acc);
+            } else
 #pragma unroll
             for (int qb = 0; qb < 8; qb += QB) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -427,6 +484,11 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             v2f acc[NR];
 #pragma unroll
             for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+            if constexpr (SP) {
+                unsigned m[1] = {si.x >> 24}, p[1] = {si.z >> 16};
+                v2f (&a1)[NR][1] = *reinterpret_cast<v2f(*)[NR][1]>(&acc);
+                sp_products<NR, 1>(Wsp, X0, m, p, kc, a1);
+            } else
 #pragma unroll
             for (int qb = 0; qb < 8; qb += QB) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -480,6 +542,13 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             for (int r = 0; r < NR; ++r)
 #pragma unroll
                 for (int j = 0; j < 3; ++j) acc[r][j] = (v2f){0.f, 0.f};
+            if constexpr (SP) {
+                const unsigned mx = si.y, pb = si.w & 0xffffu;
+                unsigned m[3] = {mx & 0xffu, (mx >> 8) & 0xffu, (mx >> 16) & 0xffu};
+                const unsigned c0 = (unsigned)__builtin_popcount(m[0]), c1 = (unsigned)__builtin_popcount(m[1]);
+                unsigned p[3] = {pb, pb + 16u * c0, pb + 16u * (c0 + c1)};
+                sp_products<NR, 3, hh2_rowmask(WIN, NR)>(Wsp, XH2, m, p, kc, acc);
+            } else
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -596,12 +665,17 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                 v2f acc[NR];
 #pragma unroll
                 for (int r = 0; r < NR; ++r) acc[r] = (v2f){0.f, 0.f};
+                if constexpr (SP) {
+                    unsigned m[1] = {si.y >> 24}, p[1] = {si.w >> 16};
+                    v2f (&a1)[NR][1] = *reinterpret_cast<v2f(*)[NR][1]>(&acc);
+                    sp_products<NR, 1>(Wsp, X0, m, p, kc, a1);
+                } else
 #pragma unroll
                 for (int qb = 0; qb < 8; qb += 4) {
                     __builtin_amdgcn_sched_barrier(0);
                     float4 wq[4];  // fc3 weights: one LDS read per step (10-bit: registers)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) wq[q] = FC3R ? wr[(32 + qb + q) % NW] : Wf[16 * (qb + q) + kc];
+                    for (int q = 0; q < 4; ++q) wq[q] = FC3R && !SP ? wr[(32 + qb + q) % NW] : Wf[16 * (qb + q) + kc];
 #pragma unroll
                     for (int r = 0; r < NR; ++r) {
                         float4 xq[4];
@@ -629,22 +703,6 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                 fc3();
             }
             float* red = lds + L_RED;
-#if WRNN_KEY_EPI
-            // [og][r] candidate keys (cand_key) of (row r, class og's), formed here by the lanes
-            // that hold the logits; (0, 0) without a class
-            if (kc < NR) {
-                CandKey k{0u, 0u};
-                if (has_cls) {
-                    const float l = p_add(s0, lds[L_BCLS + og]);
-                    p_dbg_logit<DBG>(a.dbg, t + lvm.y, lrow, cls, a.B, a.n_classes, l);
-                    if (MOL)  // MOL: logit (row kc, class cls) as a tagged pair, polled directly
-                        bst_tag(l, seq, xr, (unsigned)(kc * 32 + cls) * 8u, (XB_D + XB_D_LOG) * 4);
-                    else
-                        k = cand_key(l, __float_as_uint(pgum), cls);
-                }
-                *reinterpret_cast<uint2*>(red + (og * kPNR + kc) * 2) = make_uint2(k.hi, k.lo);
-            }
-#else
             // [og][r] (logit, noise word) of (row r, class og's); wave 0 forms the candidate keys
             // (cand_key) as it reduces them
             if (kc < NR) {
@@ -657,7 +715,6 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                 }
                 *reinterpret_cast<float2*>(red + (og * kPNR + kc) * 2) = make_float2(l, pgum);
             }
-#endif
             XSTAMP(28);
             __syncthreads();
             PSTAMP(11);
@@ -672,16 +729,10 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                         const int r = tt >> 4, o = tt & 15;
                         uint32_t bh = 0, bl = 0;
                         if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
-#if WRNN_KEY_EPI
-                            const uint2 k = *reinterpret_cast<const uint2*>(red + (o * kPNR + r) * 2);
-                            bh = k.x;
-                            bl = k.y;
-#else
                             const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
                             const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
                             bh = k.hi;
                             bl = k.lo;
-#endif
                         }
                         row16_kmax(bh, bl);
                         const int rr = r;
@@ -694,16 +745,10 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                             const int r = rb + (tt >> 5), o = tt & 31;
                             uint32_t bh = 0, bl = 0;
                             if (r < NR && o < a.cpw && a.cpw * w + o < a.n_classes) {
-#if WRNN_KEY_EPI
-                                const uint2 k = *reinterpret_cast<const uint2*>(red + (o * kPNR + r) * 2);
-                                bh = k.x;
-                                bl = k.y;
-#else
                                 const float2 lg = *reinterpret_cast<const float2*>(red + (o * kPNR + r) * 2);
                                 const CandKey k = cand_key(lg.x, __float_as_uint(lg.y), a.cpw * w + o);
                                 bh = k.hi;
                                 bl = k.lo;
-#endif
                             }
                             half_kmax(bh, bl);
                             const int rr = r;
@@ -883,7 +928,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
     }
 }
 
-template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG>
+template <int NR, bool FC3R, bool MOL, bool P1R, bool ROT, bool DBG, bool SP = false>
 __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_group, s_slot, s_ok;
@@ -901,11 +946,11 @@ __global__ __launch_bounds__(kPT, 1) void k_persist(PersistArgs a) {
     if constexpr (ROT && NR > 1) {
         // a rotated launch holds groups of NR and of NR - 1 rows: each runs its own body
         if (__builtin_amdgcn_readfirstlane(a.gnr[g]) == NR)
-            persist_body<NR, FC3R, MOL, P1R, true, DBG>(a, lds, g, w);
+            persist_body<NR, FC3R, MOL, P1R, true, DBG, SP>(a, lds, g, w);
         else
-            persist_body<NR - 1, FC3R, MOL, P1R, true, DBG>(a, lds, g, w);
+            persist_body<NR - 1, FC3R, MOL, P1R, true, DBG, SP>(a, lds, g, w);
     } else {
-        persist_body<NR, FC3R, MOL, P1R, ROT, DBG>(a, lds, g, w);
+        persist_body<NR, FC3R, MOL, P1R, ROT, DBG, SP>(a, lds, g, w);
     }
 }
 
@@ -1002,6 +1047,19 @@ size_t persist_xbuf_floats() { return (size_t)kPG * XB_GROUP; }
 
 template <int NR, bool FC3R, bool MOL, bool P1R>
 hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
+    if constexpr (P1R) {  // sparse instances (a.sparse: the pruned-weight image), ring only
+        if (a.sparse) {
+            if constexpr (!FC3R && NR >= 2)
+                if (a.vmap) {
+                    if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, true, true, true>>(persist_lds_bytes(), a, s);
+                    return persist_launch<k_persist<NR, FC3R, MOL, P1R, true, false, true>>(persist_lds_bytes(), a, s);
+                }
+            if (a.vmap) return hipErrorInvalidValue;
+            if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, false, true, true>>(persist_lds_bytes(), a, s);
+            return persist_launch<k_persist<NR, FC3R, MOL, P1R, false, false, true>>(persist_lds_bytes(), a, s);
+        }
+    }
+    if (a.sparse) return hipErrorInvalidValue;
     if constexpr (P1R && !FC3R && NR >= 2) {  // rotated launches (a.vmap): 9-bit ring variants
         if (a.vmap) {
             if (a.dbg.out) return persist_launch<k_persist<NR, FC3R, MOL, P1R, true, true>>(persist_lds_bytes(), a, s);
@@ -1013,43 +1071,53 @@ hipError_t launch_persist_t(const PersistArgs& a, hipStream_t s) {
     return persist_launch<k_persist<NR, FC3R, MOL, P1R, false, false>>(persist_lds_bytes(), a, s);
 }
 
-template <int NR, bool FC3R, bool MOL, bool P1R>
+template <int NR, bool FC3R, bool MOL, bool P1R, bool SP = false>
 int persist_spill_t() {
-    hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R, false, false>) != hipSuccess) return -1;
-    return (int)fa.localSizeBytes;
+    if constexpr (SP && !P1R) {
+        return -1;
+    } else {
+        hipFuncAttributes fa;
+        if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, FC3R, MOL, P1R, false, false, SP>) != hipSuccess) return -1;
+        return (int)fa.localSizeBytes;
+    }
 }
 
 // scratch bytes of the rotated instance (groups of NR and NR - 1 rows); -1 when none exists
-template <int NR, bool MOL>
+template <int NR, bool MOL, bool SP = false>
 int persist_rot_spill_t() {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, false, MOL, true, true, false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, (const void*)k_persist<NR, false, MOL, true, true, false, SP>) != hipSuccess) return -1;
     return (int)fa.localSizeBytes;
 }
 
 #if WRNN_PERSIST_PART != 1
-int persist_rot_scratch_mol(int nr) {
-    switch (nr) {
-        case 2: return persist_rot_spill_t<2, true>();
-        case 3: return persist_rot_spill_t<3, true>();
-        case 4: return persist_rot_spill_t<4, true>();
+int persist_rot_scratch_mol(int nr, int sparse) {
+    switch (nr * 2 + (sparse ? 1 : 0)) {
+        case 4: return persist_rot_spill_t<2, true>();
+        case 5: return persist_rot_spill_t<2, true, true>();
+        case 6: return persist_rot_spill_t<3, true>();
+        case 7: return persist_rot_spill_t<3, true, true>();
+        case 8: return persist_rot_spill_t<4, true>();
+        case 9: return persist_rot_spill_t<4, true, true>();
         default: return -1;
     }
 }
 #else
-int persist_rot_scratch_mol(int nr);
+int persist_rot_scratch_mol(int nr, int sparse);
 #endif
 
 #if WRNN_PERSIST_PART != 2
 // Scratch bytes of the rotated instance with groups of nr and nr - 1 rows (9-bit RAW or MOL,
 // P1 ring); -1 when none exists.
-int persist_rot_scratch(int nr, int mode) {
-    if (mode != 0) return persist_rot_scratch_mol(nr);
-    switch (nr) {
-        case 2: return persist_rot_spill_t<2, false>();
-        case 3: return persist_rot_spill_t<3, false>();
-        case 4: return persist_rot_spill_t<4, false>();
+int persist_rot_scratch(int nr, int mode, int sparse) {
+    if (mode != 0) return persist_rot_scratch_mol(nr, sparse);
+    switch (nr * 2 + (sparse ? 1 : 0)) {
+        case 4: return persist_rot_spill_t<2, false>();
+        case 5: return persist_rot_spill_t<2, false, true>();
+        case 6: return persist_rot_spill_t<3, false>();
+        case 7: return persist_rot_spill_t<3, false, true>();
+        case 8: return persist_rot_spill_t<4, false>();
+        case 9: return persist_rot_spill_t<4, false, true>();
         default: return -1;
     }
 }
@@ -1057,7 +1125,16 @@ int persist_rot_scratch(int nr, int mode) {
 
 #if WRNN_PERSIST_PART != 1
 // MOL variants (30 classes: cpw <= 16)
-int persist_spill_mol(int nr, int ring) {
+int persist_spill_mol(int nr, int ring, int sparse) {
+    if (sparse) {
+        switch (nr) {
+            case 1: return persist_spill_t<1, false, true, true, true>();
+            case 2: return persist_spill_t<2, false, true, true, true>();
+            case 3: return persist_spill_t<3, false, true, true, true>();
+            case 4: return persist_spill_t<4, false, true, true, true>();
+            default: return -1;
+        }
+    }
     switch (nr * 2 + (ring ? 1 : 0)) {
         case 2: return persist_spill_t<1, false, true, false>();
         case 3: return persist_spill_t<1, false, true, true>();
@@ -1086,30 +1163,33 @@ hipError_t launch_persist_mol(const PersistArgs& a, hipStream_t s) {
     }
 }
 #else
-int persist_spill_mol(int nr, int ring);
+int persist_spill_mol(int nr, int ring, int sparse);
 hipError_t launch_persist_mol(const PersistArgs& a, hipStream_t s);
 #endif
 
 #if WRNN_PERSIST_PART != 2
 template <int NR, bool P1R>
-int persist_spill_nr(int cpw, int mode) {
-    if (mode != 0) return cpw <= 16 ? persist_spill_mol(NR, P1R) : -1;  // MOL: 30 classes
+int persist_spill_nr(int cpw, int mode, int sparse) {
+    if (mode != 0) return cpw <= 16 ? persist_spill_mol(NR, P1R, sparse) : -1;  // MOL: 30 classes
+    if (sparse)
+        return !P1R ? -1 : cpw > 16 ? persist_spill_t<NR, true, false, P1R, true>()
+                                    : persist_spill_t<NR, false, false, P1R, true>();
     return cpw > 16 ? persist_spill_t<NR, true, false, P1R>() : persist_spill_t<NR, false, false, P1R>();
 }
 
-// Scratch bytes of the (rows per group, classes per slot, mode, P1 ring) variant; -1 when it
-// does not exist.
-int persist_variant_scratch(int nr, int cpw, int mode, int ring) {
+// Scratch bytes of the (rows per group, classes per slot, mode, P1 ring, sparse) variant; -1
+// when it does not exist (sparse instances: P1 ring only).
+int persist_variant_scratch(int nr, int cpw, int mode, int ring, int sparse) {
     if (cpw < 1 || cpw > kPCls) return -1;
     switch (nr * 2 + (ring ? 1 : 0)) {
-        case 2: return persist_spill_nr<1, false>(cpw, mode);
-        case 3: return persist_spill_nr<1, true>(cpw, mode);
-        case 4: return persist_spill_nr<2, false>(cpw, mode);
-        case 5: return persist_spill_nr<2, true>(cpw, mode);
-        case 6: return persist_spill_nr<3, false>(cpw, mode);
-        case 7: return persist_spill_nr<3, true>(cpw, mode);
-        case 8: return persist_spill_nr<4, false>(cpw, mode);
-        case 9: return persist_spill_nr<4, true>(cpw, mode);
+        case 2: return persist_spill_nr<1, false>(cpw, mode, sparse);
+        case 3: return persist_spill_nr<1, true>(cpw, mode, sparse);
+        case 4: return persist_spill_nr<2, false>(cpw, mode, sparse);
+        case 5: return persist_spill_nr<2, true>(cpw, mode, sparse);
+        case 6: return persist_spill_nr<3, false>(cpw, mode, sparse);
+        case 7: return persist_spill_nr<3, true>(cpw, mode, sparse);
+        case 8: return persist_spill_nr<4, false>(cpw, mode, sparse);
+        case 9: return persist_spill_nr<4, true>(cpw, mode, sparse);
         default: return -1;
     }
 }
@@ -1117,7 +1197,7 @@ int persist_variant_scratch(int nr, int cpw, int mode, int ring) {
 // 1 when the variant exists and keeps its state in registers (no scratch spills: scratch
 // traffic would serialise behind every exchange).
 int persist_variant_ok(int nr, int cpw, int mode, int ring) {
-    return persist_variant_scratch(nr, cpw, mode, ring) == 0 ? 1 : 0;
+    return persist_variant_scratch(nr, cpw, mode, ring, 0) == 0 ? 1 : 0;
 }
 
 template <int NR, bool P1R>

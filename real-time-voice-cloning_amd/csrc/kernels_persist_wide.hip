@@ -190,9 +190,6 @@ __device__ __forceinline__ bool w_poll(rsrc_t xr, unsigned voff, unsigned so, bo
 //      first tile's MFMAs -- the registers hold the other nine tiles; its partials go to PH after
 //      one more barrier (the gh1 / gh2 partial sums are read in the hop-C wait instead of hop D,
 //      so PH is free by then)
-#ifndef WRNN_FC3B_POL
-#define WRNN_FC3B_POL 0  // cache policy of the second fc3 tile's loads (A/B: 2 = non-temporal)
-#endif
 template <bool ROT, bool C10, bool DBG>
 __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // the whole 160 KiB
@@ -644,7 +641,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 fb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(fr, (unsigned)ll * 16u,
-                                                                                         (unsigned)q * 1024u, WRNN_FC3B_POL));
+                                                                                         (unsigned)q * 1024u, 0));
         }
         if constexpr (!C10) prefetch_d();
         WSTAMP(8);
@@ -672,7 +669,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide(PersistArgs a) {
         wbar();
         WSTAMP(9);
         if (lo) {
-            // fc3 epilogue: the candidate key (persist_common.h cand_key: l_k + G_k in float64)
+            // fc3 epilogue: the candidate key (cand_key.h: l_k + G_k formed exactly as an fp32 pair)
             // of the slot's 16 classes per row, max over the row's DPP row of 16 lanes,
             // published with the step tag by lane cul == 0
             {

@@ -654,7 +654,7 @@ __global__ __launch_bounds__(kPT, 1) void k_persist_wide_rr(PersistRRArgs a) {
             if (v < 4) {
                 const unsigned want = key_tag(seq);
                 {
-                    // candidate: the max key (persist_common.h cand_key, l_k + G_k formed exactly)
+                    // candidate: the max key (cand_key.h cand_key, l_k + G_k formed exactly)
                     // over the slot's classes of row cn: lane cul takes classes cpw s + 16 j + cul,
                     // j < ntc
                     uint32_t kh = 0, kl = 0;

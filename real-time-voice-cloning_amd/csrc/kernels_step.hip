@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kThreads) void k_sample(SampleArgs a) {
     float x = 0.f;
     if (a.t >= 0) {
         if (a.mode == 0) {
-            // 2. the decision (persist_common.h cand_key, the same as the persistent kernels'):
+            // 2. the decision (cand_key.h cand_key, the same as the persistent kernels'):
             //    argmax_k (l_k + G_k), G_k = -log q_k of the contract's Exp(1) variate (philox.h
             //    gumbel_q_of, computed while the logits are in flight), l + G formed exactly --
             //    the reference's argmax((softmax(l) / sum) / q) without fp32 rounding of its own

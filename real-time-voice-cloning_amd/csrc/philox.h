@@ -49,7 +49,7 @@ __host__ __device__ inline float gumbel_of(uint32_t x) {
 // nearest integer: q lies in [5.96e-8, 16.64], so G + 4 in [1.19, 20.64] and the word < 2^32;
 // the quantisation error is <= 2^-28 = 3.7e-9 absolute -- below even the last fp32 division of
 // the reference's own p / q (2^-24 relative) -- and the noise still costs 4 bytes per class.
-// persist_common.h cand_key adds it to the fp32 logit in float64.
+// cand_key.h adds it to the fp32 logit exactly, as an fp32 pair (TwoSum, then Fast2Sum).
 constexpr double kGumbelOffset = 4.0;
 constexpr double kGumbelScale = 134217728.0;  // 2^27
 __host__ __device__ inline uint32_t gumbel_q_of(uint32_t x) {

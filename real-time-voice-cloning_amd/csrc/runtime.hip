@@ -2189,6 +2189,12 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     const bool rotp = nb > 0 && h->p_plan[0].rot >= 0;
     std::vector<size_t> rot_off;  // per launch: byte offset of its block
     if (rotp) {
+        // a rotated launch's block holds kPG * nr_hi row slots and the kernel runs L.nr rows:
+        // they must agree (generate_impl plans the rotation only then)
+        for (const auto& L : h->p_plan)
+            if (!L.wide && L.nr != RP.nr_hi)
+                return fail(WRNN_ERR_INVALID, "rotated launch with " + std::to_string(L.nr) +
+                                                   " rows per group, rotation plan of " + std::to_string(RP.nr_hi));
         auto nv_of = [&](const wrnn_handle::PLaunch& L) { return kPG * (L.wide ? h->wrot[L.rot].nr : RP.nr_hi); };
         size_t total = 0;
         for (const auto& L : h->p_plan) {
@@ -2480,7 +2486,9 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
 // per-step cost of a runtimeracer wide-row launch at 1 row per group, for the launch plan
 // (MI355X, bench HIP events)
 static const double kWideRRUs = 12.0;  // 12.39 us at 15-16 rows (profiles/r04/wide_rr/)
-static const double kWide10Us = 0.8;   // fatchord wide, 1024 classes: the second fc3 tile (estimate)
+// fatchord wide, 1024 classes: the second fc3 tile -- measured 10.965 us per launch step at 16
+// rows per group (b10) against 9.724 at 512 classes (c4), profiles/r05/final/{b10,c4}.log
+static const double kWide10Us = 1.24;
 
 int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
@@ -2688,18 +2696,23 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // row rotation (plan_rotation): one register-resident 9-bit launch with
     // uneven groups becomes K launches over rotating row sets (WRNN_PERSIST_ROT=0: off)
     h->rot_plan = wrnn_handle::RotPlan();
-    const bool fat_rot = use_p && h->p1_ring && h->p_plan.size() == 1 && !h->p_plan[0].wide && !h->pw.rr &&
+    // plan_rotation derives its (q + 1)-row body from B: the single launch must run exactly
+    // ceil(B / 8) rows per group (a WRNN_PERSIST_NR_MAX cap or a spill-filtered variant can
+    // leave it at another count, and the rotated layout would then misread its row slots)
+    const bool rot_nr = use_p && h->p_plan.size() == 1 && h->p_plan[0].nr == (B + kPG - 1) / kPG;
+    // every rotated kernel forms its noise offsets ((step offset x Bp + row) x n + class) x 4 in
+    // 32 bits: the padded noise stream must stay below 4 GB
+    const bool rot_off32 = (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
+    const bool fat_rot = use_p && rot_nr && rot_off32 && h->p1_ring && !h->p_plan[0].wide && !h->pw.rr &&
                          !h->pw.gen && h->pw.cpw <= 16 &&
                          (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
     // runtimeracer (k_persist_rr, RAW / MOL): P1 and the noise from their streams at each row's own
     // step (the noise stream addressed with 32-bit offsets: < 4 GiB)
-    const bool rr_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.rr &&
-                        (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2 &&
-                        (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
+    const bool rr_rot = use_p && rot_nr && rot_off32 && !h->p_plan[0].wide && h->pw.rr &&
+                        (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2;
     // geneing (k_persist_gen, categorical 'BITS' and MOL): as runtimeracer
-    const bool gen_rot = use_p && h->p_plan.size() == 1 && !h->p_plan[0].wide && h->pw.gen &&
-                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) &&
-                         h->p_plan[0].nr >= 2 && (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
+    const bool gen_rot = use_p && rot_nr && rot_off32 && !h->p_plan[0].wide && h->pw.gen &&
+                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2;
     if (fat_rot || rr_rot || gen_rot) {
         const char* env = std::getenv("WRNN_PERSIST_ROT");
         const int nr = h->p_plan[0].nr;

@@ -178,6 +178,10 @@ constexpr int kPPhases = 32; // diagnostic stamps per workgroup per traced step
 inline int persist_reg_f4(int cpw) { return cpw > 16 ? 40 : 32; }
 // LDS weights per slot (float4): W_hh2 [16 units][3][kPK4], then fc3 [16 classes][kPK4]
 constexpr int kPLdsW4 = 16 * 3 * kPK4 + 16 * kPK4;
+// Sparse instances (pruned weights): the slot's live 1 x 4 blocks as
+// per-(set, output row) lists in the same kPLdsW4 float4; its last 16 float4 stay zero (the
+// row a lane with no block left reads), so the lists hold at most kPSpZero float4
+constexpr int kPSpZero = kPLdsW4 - 16;
 
 // control words (zeroed by the host before every launch); PC_ERR: 1 registration timeout,
 // 2 exchange timeout, 3 workgroups not spread 32 per XCD
@@ -248,6 +252,9 @@ struct PersistArgs {
     const int2* vmap;
     const int* gnr;
     const int* giters;
+    // sparse instance (k_persist only; P1 ring): wreg = [kPM][kPT] uint4 per-lane masks / list
+    // bases, wlds = [kPM][kPLdsW4] float4 block lists (runtime.hip pack_persist_sparse)
+    int sparse;
 };
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
@@ -405,8 +412,9 @@ hipError_t launch_gumbel_rows(float* g, int S, int r0, int nrows, int ld, int n_
                               const RowInfo* rows, uint32_t k0, uint32_t k1, hipStream_t s);
 // ring: the P1-ring variant (PersistArgs::p1q set) or the P1-stream variant
 int persist_variant_ok(int nr, int cpw, int mode, int ring);
-int persist_variant_scratch(int nr, int cpw, int mode, int ring);
-int persist_rot_scratch(int nr, int mode);  // rotated instance (groups of nr and nr - 1 rows)
+int persist_variant_scratch(int nr, int cpw, int mode, int ring, int sparse = 0);
+// rotated instance (groups of nr and nr - 1 rows)
+int persist_rot_scratch(int nr, int mode, int sparse = 0);
 size_t persist_lds_bytes();
 size_t persist_xbuf_floats();
 

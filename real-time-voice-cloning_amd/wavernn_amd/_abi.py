@@ -150,12 +150,19 @@ def load_library(path=None):
     }
     # (an A/B build given by WRNN_LIB may predate an entry point: it is left unbound)
     tolerant = host_only or bool(os.environ.get('WRNN_LIB'))
+    unbound = []
     for name, (res, args) in sig.items():
         if tolerant and not hasattr(lib, name):
+            unbound.append(name)
             continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if unbound and not host_only:
+        # a stale or wrong WRNN_LIB says so at load time, not as an AttributeError deep in a run
+        import warnings
+        warnings.warn(f'{path}: {len(unbound)} entry points missing, left unbound: '
+                      + ', '.join(sorted(unbound)), RuntimeWarning, stacklevel=2)
     if path == LIB_PATH:
         _lib = lib
     return lib

@@ -34,9 +34,13 @@ def golden_case(name):
 def state_dict_of(meta):
     """The fixture's seeded weights (synth_state_dict with the case's statistics knobs)."""
     from wavernn_amd.synth import synth_state_dict
-    return synth_state_dict(hparams_of(meta), meta['model_type'], seed=meta['weight_seed'],
-                            logit_scale=meta['logit_scale'], gru_scale=meta.get('gru_scale', 1.0),
-                            fc_scale=meta.get('fc_scale', 1.0))
+    sd = synth_state_dict(hparams_of(meta), meta['model_type'], seed=meta['weight_seed'],
+                          logit_scale=meta['logit_scale'], gru_scale=meta.get('gru_scale', 1.0),
+                          fc_scale=meta.get('fc_scale', 1.0))
+    if meta.get('prune'):  # pruned checkpoints: the reference Pruner's masks (wavernn_amd.prune)
+        from wavernn_amd.prune import prune_state_dict
+        sd = prune_state_dict(sd, meta['model_type'], z=meta['prune'], group=4)
+    return sd
 
 
 def wave_equal(wav, gold):

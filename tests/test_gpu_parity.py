@@ -52,8 +52,6 @@ def engine_cases(continuous):
     for k, v in golden_meta().items():
         if is_continuous(v) != continuous:
             continue
-        if v.get('gru_scale', 1.0) != 1.0:  # trained-like: test_gpu_trained.py (near-tie analysis)
-            continue
         out.append((k, 'chain'))
         out.append((k, 'persist'))
     return out
@@ -68,6 +66,25 @@ def test_raw_labels_and_wave_bit_exact(name, engine):
     meta, gold, m, wav = run_case(name, engine)
     lab = m.last_labels
     assert lab.shape == gold['labels'].shape == (meta['num_folds'], meta['seq_len'])
+    if meta.get('gru_scale', 1.0) != 1.0:
+        # trained-like fixtures (peaked posteriors, |logit| ~ 20) on the engine's DEFAULT plan:
+        # bit-exact, or measured near-ties in no more folds than measured (test_gpu_trained.py)
+        from test_gpu_trained import near_tie_gate
+
+        def rerun(steps):
+            m2, _, _ = make_model(meta)
+            m2.set_engine(engine)
+            m2.set_debug_steps(steps)
+            from wavernn_amd.hparams import sp
+            from wavernn_amd.synth import synth_mel
+            mel = synth_mel(meta['n_frames'], meta['mel_seed']) / sp.max_abs_value
+            m2.generate(mel[None], meta['batched'], meta['target'], meta['overlap'],
+                        hparams_of(meta).mu_law, sp.preemphasize, progress_callback=lambda *a: None)
+            return m2
+        names = [st[0] for st in m.stage_info()]
+        kind = engine if engine == 'chain' else ('wide' if 'persist_wide' in names else 'persist')
+        near_tie_gate(name, kind, meta, gold, lab, wav, rerun)
+        return
     agree = float((lab == gold['labels']).mean())
     assert agree == 1.0, f'{name}/{engine}: label agreement {agree}, first divergence (row, step) ' \
                          f'{first_divergence(lab, gold["labels"])}'
