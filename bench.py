@@ -48,16 +48,21 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=15.0,
                     help='CPU-baseline sample budget (0 disables)')
     ap.add_argument('--no-timing', action='store_true', help='disable kernel timing')
+    ap.add_argument('--prune', type=float, default=0.0,
+                    help='prune the synthetic weights as the reference Pruner does at this '
+                         'sparsity in 1x4 groups (vocoder/pruner.py; 0.9 = its target): the '
+                         'block-sparse kernels run them (DESIGN.md §3.0g)')
     ap.add_argument('--engine', default='auto', choices=['auto', 'chain', 'persist'],
                     help='recurrence engine (include/wavernn_mi355x.h WRNN_ENGINE_*)')
     return ap.parse_args()
 
 
-def workload_of(utts, frames, model, wname, target, overlap):
+def workload_of(utts, frames, model, wname, target, overlap, prune=0.0):
     """The line's config.workload string; also the key under which tools/pmc_traffic.py files
     the counters of a workload (with the kernel name)."""
     return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
-            f'batched folds target={target} overlap={overlap}')
+            f'batched folds target={target} overlap={overlap}' +
+            (f', weights pruned {prune:.2f} in 1x4 blocks' if prune else ''))
 
 
 def _pmc_traffic(kernel, workload):
@@ -289,6 +294,9 @@ def main():
 
     hp = hparams_for(args.model).copy(bits=args.bits, mode=args.mode)  # geneing RAW = Beta
     sd = synth_state_dict(hp, args.model, seed=0)
+    if args.prune:
+        from wavernn_amd.prune import prune_state_dict
+        sd = prune_state_dict(sd, args.model, z=args.prune, group=4)
     model = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
                     hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
                     mode=hp.mode, model_type=args.model, device=local)
@@ -356,7 +364,8 @@ def main():
 
     wname = ('MOL' if hp.mode == 'MOL' else 'RAW (Beta)' if args.model == 'geneing-wavernn' and hp.mode == 'RAW'
              else f'{args.mode} {args.bits}-bit' + (' mu-law' if hp.mu_law else ''))
-    workload = workload_of(U, args.frames, args.model, wname, args.target, args.overlap)
+    workload = workload_of(U, args.frames, args.model, wname, args.target, args.overlap, args.prune)
+    spi = model.sparse_info()
     roof = None
     us_rank = None
     info = model.stage_info() if not args.no_timing else []
@@ -373,6 +382,8 @@ def main():
         achieved = by / (us * 1e-6) / 1e9 if us > 0 else None
         sfx = {'runtimeracer-wavernn': '_rr', 'geneing-wavernn': '_gen'}.get(args.model, '')
         kernel = {'persist': 'k_persist' + sfx, 'persist_wide': 'k_persist_wide' + sfx}.get(name, f'k_stage<{name}>')
+        if name == 'persist' and spi['last_call']:
+            kernel = 'k_persist (sparse)'  # the SP instances (pruned weights)
         roof = {'bound': 'hbm', 'kernel': kernel, 'achieved': achieved,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': (achieved / HBM_PEAK_GBS) if achieved else None, 'traffic': None,
@@ -466,6 +477,8 @@ def main():
                                    f'to rank 0 (RCCL gather), f64 post-processing on rank 0'
                                    if world > 1 else 'one GPU'),
                    'engine': model.last_engine(), 'persist_fallbacks': fb[0],
+                   'sparse': {'prune': args.prune, 'image': spi['available'], 'ran': spi['last_call'],
+                              'live_block_fraction': spi['density'], 'lds_list_fill_f4': spi['fill_f4']},
                    'lib_build': lib_build_id()},
         'roofline': roof,
         'cpu_baseline': None,

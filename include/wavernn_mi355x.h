@@ -178,6 +178,14 @@ int wrnn_last_engine(wrnn_handle* h, int* engine);
  * warning to stderr; with WRNN_ENGINE_PERSIST requested the call fails instead. AUTO stops
  * trying PERSIST after 3 failed calls in a row. */
 int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_cap);
+/* Block-sparse execution of pruned checkpoints (the reference's Pruner, vocoder/pruner.py:60-88;
+ * its native backend's sparse GEMV, vocoder/libwavernn/runtimeracer_version/src/wavernn.cpp:
+ * 162-184): *available = the loaded fatchord weights have a sparse k_persist image (their live
+ * 1 x 4 blocks fit the kernel's LDS lists); *last_call = the last call's register-resident
+ * launches ran it; *density = live fraction of the step matrices' 1 x 4 blocks; *fill_f4 = the
+ * fullest slot's list size (float4). Results equal the dense kernels' bit for bit. Env
+ * WRNN_SPARSE=0 turns it off. Any pointer may be null. */
+int wrnn_sparse_info(wrnn_handle* h, int* available, int* last_call, double* density, int* fill_f4);
 /* Launch plan of the last PERSIST call (operator introspection; no reference equivalent):
  * *n_launches launches; for i < n_launches, launch i runs fold rows first_row[i] + g + 8 r,
  * r < rows_per_group[i], on the wide MFMA kernel when wide[i] != 0. Arrays may be null;

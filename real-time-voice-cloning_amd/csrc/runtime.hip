@@ -180,6 +180,7 @@ struct wrnn_handle {
     bool melup_valid = false;  // ws.melup holds the last call's upsampled mel (not per-frame P1)
     bool p1_ring = false;      // this call's k_persist launches form P1 in-kernel
     bool p1_stream = false;    // this call writes the [S][B][4H] P1 stream (other kernels)
+    bool sparse_call = false;  // this call's k_persist launches run the sparse instances
     bool timing = false;
     int phase_step = -1;  // diagnostic (env WRNN_PHASE_STEP): per-phase stamps of one step
     DevBuf phases;
@@ -205,6 +206,14 @@ struct wrnn_handle {
         const float *wwide = nullptr, *wwide_lds = nullptr;  // wide-row launches (MFMA images)
         const float* wfc3b = nullptr;  // ... > 512 classes: the second fc3 tile (L2-streamed)
         const float* wwide_rr = nullptr;  // runtimeracer wide-row launches (kernels_persist_wide_rr.hip)
+        // sparse k_persist image (pruned checkpoints, pack_persist_sparse):
+        // per-lane masks / list bases [kPM][kPT] uint4 and the block lists [kPM][kPLdsW4] float4
+        bool sp_ok = false;
+        const float *swreg = nullptr, *swlds = nullptr;
+        double sp_density = 1.0;   // live fraction of the kernel's 1 x 4 weight blocks
+        int sp_fill = 0;           // float4 of the fullest slot's lists (of kPSpZero)
+        double sp_live_bytes = 0;  // live step-weight bytes (blocks x 16 B + a 2-byte index each)
+        double sp_live_macs = 0;   // live MACs per row-step of the pruned step matrices
         const float *b_hh1 = nullptr, *b_hh2 = nullptr, *b_fc3 = nullptr;  // rr: b_fc3 = fc5 bias
         const float *b_ih2 = nullptr, *b_ih4 = nullptr, *b_hh3 = nullptr, *b_hh4 = nullptr,
                     *b_f2 = nullptr, *b_f4 = nullptr;  // rr only
@@ -559,6 +568,8 @@ int pack_p1(wrnn_handle* h, bool x4) {
 int pack_persist_wide(wrnn_handle* h);
 int pack_persist_wide_rr(wrnn_handle* h);
 
+int pack_persist_sparse(wrnn_handle* h);
+
 int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     auto& T = h->host;
     const int H = h->H, F = h->F, A = h->A, n = h->n_classes;
@@ -631,6 +642,121 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
     P.oF1 = oF1;
     P.oF2 = oF2;
     P.ok = true;
+    return pack_persist_sparse(h);
+}
+
+// Sparse image of the fatchord step weights (kernels_persist.hip sp_products).
+// A pruned checkpoint (vocoder/pruner.py:60-88: 1 x 4 column groups zeroed, prune_layers at
+// fatchord_version.py:115) carries its masks as zeros; this finds the live blocks of every
+// product a k_persist lane owns -- the blocks of its dense register / LDS float4 -- and lists
+// them per (product set, 16-lane row group), entry e of lane kc at base + 16 e:
+//   A  (mask bits 8 j + q): og < 16 W_ih2[:, :512] rows j H + u, og >= 16 W_hh1 rows j H + u
+//   F  (8 bits): og < 16 fc2 row u, og >= 16 fc1 row u          (x parts)
+//   H  (24 bits): W_hh2 rows j H + 16 w + (og & 15) -- both halves of the workgroup read the
+//      same list (hops B / C / D split its rows, not its weights)
+//   C  (8 bits): fc3 class cpw w + og, og < cpw
+// with q the dense kernel's block index (columns 4 (16 q + kc) .. + 3). The image exists when
+// every slot's lists fit kPSpZero float4 (90 %-pruned fatchord: ~20 %); otherwise the dense
+// kernels run the zeros (same results, no sparse speed).
+int pack_persist_sparse(wrnn_handle* h) {
+    auto& T = h->host;
+    auto& P = h->pw;
+    P.sp_ok = false;
+    P.swreg = P.swlds = nullptr;
+    P.sp_density = 1.0;
+    P.sp_fill = 0;
+    const int H = h->H, F = h->F, A = h->A, n = h->n_classes, cpw = P.cpw;
+    const auto& Wih2 = T["rnn2.weight_ih_l0"];
+    const auto& Whh1 = T["rnn1.weight_hh_l0"];
+    const auto& Whh2 = T["rnn2.weight_hh_l0"];
+    const auto& Wf1 = T["fc1.weight"];
+    const auto& Wf2 = T["fc2.weight"];
+    const auto& Wf3 = T["fc3.weight"];
+    auto zero4 = [](const float* p) { return p[0] == 0.f && p[1] == 0.f && p[2] == 0.f && p[3] == 0.f; };
+    // the block (row pointer, column block q of lane kc) of each set
+    auto blkA = [&](int w, int og, int kc, int j, int q) -> const float* {
+        const int u = 16 * w + (og & 15), row = j * H + u, k0 = 4 * (16 * q + kc);
+        return og < 16 ? &Wih2[(size_t)row * (H + A) + k0] : &Whh1[(size_t)row * H + k0];
+    };
+    auto blkF = [&](int w, int og, int kc, int q) -> const float* {
+        const int u = 16 * w + (og & 15), k0 = 4 * (16 * q + kc);
+        return og < 16 ? &Wf2[(size_t)u * (F + A) + k0] : &Wf1[(size_t)u * (H + A) + k0];
+    };
+    auto blkH = [&](int w, int ul, int kc, int j, int q) -> const float* {
+        return &Whh2[(size_t)(j * H + 16 * w + ul) * H + 4 * (16 * q + kc)];
+    };
+    auto blkC = [&](int w, int og, int kc, int q) -> const float* {
+        return &Wf3[(size_t)(cpw * w + og) * F + 4 * (16 * q + kc)];
+    };
+    std::vector<uint32_t> info((size_t)kPM * kPT * 4, 0u);
+    std::vector<float> img((size_t)kPM * kPLdsW4 * 4, 0.f);
+    long long live = 0, total = 0;
+    double live_macs = 0;
+    for (int w = 0; w < kPM; ++w) {
+        float* L = img.data() + (size_t)w * kPLdsW4 * 4;
+        int top = 0;  // float4 used in this slot
+        // one set: per row group og (16 lanes), the lanes' masks, then the lists at `top`
+        auto put_set = [&](int og_lo, int og_hi, int nbits, auto blk, int word, int shift, int bword, int bshift,
+                           int row_groups_ok) {
+            for (int og = og_lo; og < og_hi; ++og) {
+                if (!row_groups_ok) continue;
+                uint32_t mk[16];
+                int cap = 0;
+                for (int kc = 0; kc < 16; ++kc) {
+                    uint32_t m = 0;
+                    for (int b = 0; b < nbits; ++b) {
+                        ++total;
+                        if (!zero4(blk(og, kc, b))) {
+                            m |= 1u << b;
+                            ++live;
+                        }
+                    }
+                    mk[kc] = m;
+                    cap = std::max(cap, __builtin_popcount(m));
+                }
+                if (top + 16 * cap > kPSpZero) return false;
+                for (int kc = 0; kc < 16; ++kc) {
+                    int e = 0;
+                    for (int b = 0; b < nbits; ++b)
+                        if (mk[kc] >> b & 1u) std::memcpy(L + ((size_t)top + 16 * e++ + kc) * 4, blk(og, kc, b), 16);
+                    const int tid = og * 16 + kc;
+                    uint32_t* in = &info[((size_t)w * kPT + tid) * 4];
+                    in[word] |= mk[kc] << shift;
+                    in[bword] |= (uint32_t)(top + kc) << bshift;
+                    if (word == 1 && shift == 0) {  // H: the other half of the workgroup reads it too
+                        uint32_t* in2 = &info[((size_t)w * kPT + tid + 256) * 4];
+                        in2[word] |= mk[kc] << shift;
+                        in2[bword] |= (uint32_t)(top + kc) << bshift;
+                    }
+                }
+                top += 16 * cap;
+            }
+            return true;
+        };
+        bool ok = put_set(0, 32, 24, [&](int og, int kc, int b) { return blkA(w, og, kc, b / 8, b % 8); }, 0, 0, 2, 0, 1) &&
+                  put_set(0, 32, 8, [&](int og, int kc, int b) { return blkF(w, og, kc, b); }, 0, 24, 2, 16, 1) &&
+                  put_set(0, 16, 24, [&](int og, int kc, int b) { return blkH(w, og, kc, b / 8, b % 8); }, 1, 0, 3, 0, 1);
+        if (ok)
+            for (int og = 0; og < std::min(cpw, 32) && ok; ++og)
+                ok = put_set(og, og + 1, 8, [&](int o, int kc, int b) { return blkC(w, o, kc, b); }, 1, 24, 3, 16,
+                             cpw * w + og < n);
+        if (!ok) return WRNN_OK;  // a slot's lists exceed the LDS carve: dense kernels only
+        P.sp_fill = std::max(P.sp_fill, top);
+    }
+    // live MACs per row-step of the pruned step matrices the kernel multiplies (x parts; the aux
+    // parts and I are in the per-frame / conditioning GEMMs)
+    live_macs = 4.0 * (double)live;
+    P.sp_density = total ? (double)live / (double)total : 1.0;
+    P.sp_live_macs = live_macs;
+    P.sp_live_bytes = (double)live * 18.0;
+    int rc = WRNN_OK;
+    std::vector<float> infof(info.size());  // (the words' bits, moved as bytes)
+    std::memcpy(infof.data(), info.data(), info.size() * sizeof(uint32_t));
+    P.swreg = upload(h, infof, &rc);
+    CHECK(rc);
+    P.swlds = upload(h, img, &rc);
+    CHECK(rc);
+    P.sp_ok = true;
     return WRNN_OK;
 }
 
@@ -2025,8 +2151,9 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     a.hop = h->hop;
     a.cpw = W.cpw;
     a.rows = (const RowInfo*)ws.rows.p;
-    a.wreg = (const float4*)W.wreg;
-    a.wlds = (const float4*)W.wlds;
+    a.wreg = (const float4*)(h->sparse_call ? W.swreg : W.wreg);
+    a.wlds = (const float4*)(h->sparse_call ? W.swlds : W.wlds);
+    a.sparse = h->sparse_call ? 1 : 0;
     a.b_hh1 = W.b_hh1;
     a.b_hh2 = W.b_hh2;
     a.b_fc3 = W.b_fc3;
@@ -2418,6 +2545,14 @@ int run_persist(wrnn_handle* h, int S, wrnn_progress_fn cb, void* user) {
     h->p_wbytes = 4.0 * wparams;
     h->p_row_bytes = (h->feat + h->R) * 4.0 + 2.0;
     h->p_macs = macs;
+    if (h->sparse_call) {
+        // sparse launches: the live blocks of the step matrices (16 B + a 2-byte index each)
+        // replace their dense bytes / MACs; the rest (I, the aux columns, biases) unchanged
+        double dense_k = 0;  // dense params of the matrices pack_persist_sparse lists
+        dense_k = 3.0 * kPH * kPH * 3 + 2.0 * kPH * kPH + (double)h->n_classes * kPH;
+        h->p_wbytes += W.sp_live_bytes - 4.0 * dense_k;
+        h->p_macs += W.sp_live_macs - dense_k;
+    }
     h->pstages.clear();
     for (const auto& L : h->p_plan) {
         int real = std::max(0, std::min(B, L.rb + kPG * L.nr) - L.rb);
@@ -2554,6 +2689,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // rows + one launch at 2 rows.
     std::vector<wrnn_handle::PLaunch> lplan;
     double plan_us = 0;  // the plan's summed per-step cost (us), for the time-sliced alternative
+    // sparse k_persist instances (pruned checkpoints): when the model's image
+    // exists (pack_persist_sparse) and the call can form P1 in the ring; env WRNN_SPARSE=0 off
+    // (A/B: the dense kernels run the same zeros to the same results)
+    bool sp = h->pw.sp_ok && !h->pw.rr && !h->pw.gen && p1_ring_ok(h) &&
+              (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
+    if (const char* e = std::getenv("WRNN_SPARSE"))
+        if (!std::strcmp(e, "0")) sp = false;
     if (h->pw.ok) {
         struct Opt {
             int nr;
@@ -2565,8 +2707,16 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             // measured MI355X us per step by rows per group (9-bit: round 5, tools/nr_probe.sh;
             // 10-bit: round 2)
             static const double us[2][kPNR + 1] = {{0, 4.8, 5.15, 5.91, 6.92}, {0, 4.9, 5.64, 7.7, 9.4}};
+            // sparse instances at ~10 % density: no register weights, so every row count is
+            // spill-free (estimates until measured, §3.0g)
+            static const double us_sp[2][kPNR + 1] = {{0, 4.6, 4.9, 5.4, 6.0}, {0, 4.7, 5.1, 5.7, 6.4}};
             const int w10 = h->pw.cpw > 16 ? 1 : 0;
             for (int c = 1; c <= kPNR; ++c) {
+                if (sp) {
+                    const int ss = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 1, 1);
+                    if (ss >= 0 && ss <= 64) opts.push_back({c, false, us_sp[w10][c]});
+                    continue;
+                }
                 int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 0);
                 if (p1_ring_ok(h)) {  // the call uses the flavour that spills less (below)
                     const int sr = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 1);
@@ -2688,11 +2838,18 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // the stream (measured: MOL at 3 rows per group spills one register with the ring and
     // runs 6.87 against 6.53 us per step)
     h->p1_ring = use_p && p1_ring_ok(h);
-    for (const auto& L : h->p_plan)
-        if (h->p1_ring && !L.wide &&
-            persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
-                persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
-            h->p1_ring = false;
+    h->sparse_call = false;
+    bool any_reg = false;
+    for (const auto& L : h->p_plan) any_reg |= !L.wide;
+    if (use_p && sp && any_reg) {
+        h->sparse_call = true;  // (sparse instances exist with the ring only: it stays on)
+    } else {
+        for (const auto& L : h->p_plan)
+            if (h->p1_ring && !L.wide &&
+                persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
+                    persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
+                h->p1_ring = false;
+    }
     // row rotation (plan_rotation): one register-resident 9-bit launch with
     // uneven groups becomes K launches over rotating row sets (WRNN_PERSIST_ROT=0: off)
     h->rot_plan = wrnn_handle::RotPlan();
@@ -2720,11 +2877,13 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         // single-launch rate, the q-row one a little slower than its own kernel (2 rows: 5.22
         // against 5.15 us -- the best split measured)
         static const double us9[kPNR + 1] = {0, 4.8, 5.22, 5.91, 6.92};
-        double t_hi = nr >= 1 ? us9[nr] : 0, t_lo = nr >= 2 ? us9[nr - 1] : 0;
+        static const double us9s[kPNR + 1] = {0, 4.6, 4.9, 5.4, 6.0};  // sparse (estimates, §3.0g)
+        const double* u9 = h->sparse_call ? us9s : us9;
+        double t_hi = nr >= 1 ? u9[nr] : 0, t_lo = nr >= 2 ? u9[nr - 1] : 0;
         // MOL: its rotated 3-row body (one spilled register) runs much slower than the 2-row
         // one -- the split balanced for 5.91 / 4.70 is the fastest of a scan from 5.22 down to
         // 4.55 (C3 5.61 -> 5.19 us per step; DESIGN.md §3.0e, profiles/r05/rotation/)
-        if (h->cfg.mode == WRNN_MODE_MOL && nr == 3) t_lo = 4.70;
+        if (h->cfg.mode == WRNN_MODE_MOL && nr == 3 && !h->sparse_call) t_lo = 4.70;
         if (rr_rot) {  // runtimeracer, measured single-launch step times at 1-4 rows per group
             static const double rr9[kPNR + 1] = {0, 6.3, 7.0, 7.78, 8.8};   // 9-bit (2 / 4 rows: estimates)
             static const double rr10[kPNR + 1] = {0, 6.5, 7.26, 8.14, 9.23};  // 10-bit (profiles/r05/rr_rates/)
@@ -2751,7 +2910,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
         // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
         const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr, h->cfg.mode == WRNN_MODE_MOL)
-                     : gen_rot ? persist_gen_rot_scratch(nr, h->cfg.mode) : persist_rot_scratch(nr, h->cfg.mode);
+                     : gen_rot ? persist_gen_rot_scratch(nr, h->cfg.mode)
+                               : persist_rot_scratch(nr, h->cfg.mode, h->sparse_call ? 1 : 0);
         if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
             plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
             h->p_plan.clear();
@@ -3186,6 +3346,15 @@ int wrnn_plan_info(wrnn_handle* h, int* n_launches, int* first_row, int* rows_pe
         if (rows_per_group) rows_per_group[i] = h->p_plan[i].nr;
         if (wide) wide[i] = h->p_plan[i].wide ? 1 : 0;
     }
+    return WRNN_OK;
+}
+
+int wrnn_sparse_info(wrnn_handle* h, int* available, int* last_call, double* density, int* fill_f4) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (available) *available = h->pw.sp_ok ? 1 : 0;
+    if (last_call) *last_call = h->last_engine == WRNN_ENGINE_PERSIST && h->sparse_call ? 1 : 0;
+    if (density) *density = h->pw.sp_density;
+    if (fill_f4) *fill_f4 = h->pw.sp_fill;
     return WRNN_OK;
 }
 

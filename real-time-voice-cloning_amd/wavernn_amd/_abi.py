@@ -130,6 +130,7 @@ def load_library(path=None):
                                        c_void_p, c_size_t]),
         'wrnn_debug_noise': (c_int, [c_void_p, c_int, P(ctypes.c_float), c_size_t]),
         'wrnn_plan_info': (c_int, [c_void_p, P(c_int), P(c_int), P(c_int), P(c_int), c_int]),
+        'wrnn_sparse_info': (c_int, [c_void_p, P(c_int), P(c_int), P(ctypes.c_double), P(c_int)]),
         'wrnn_debug_beta': (c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.c_uint32, ctypes.c_float, ctypes.c_float,
                                     P(ctypes.c_float)]),

@@ -227,6 +227,18 @@ class WaveRNN:
         _abi.check(self._lib.wrnn_persist_steps(self._h, int(stage), ctypes.byref(v)))
         return v.value
 
+    def sparse_info(self):
+        """Block-sparse execution (pruned checkpoints): dict(available,
+        last_call, density, fill_f4) -- whether the loaded weights have a sparse image, whether
+        the last call ran it, the live fraction of the step matrices' 1 x 4 blocks, and the
+        fullest slot's LDS list size."""
+        av, lc, fill = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        d = ctypes.c_double()
+        _abi.check(self._lib.wrnn_sparse_info(self._h, ctypes.byref(av), ctypes.byref(lc),
+                                              ctypes.byref(d), ctypes.byref(fill)))
+        return dict(available=bool(av.value), last_call=bool(lc.value), density=d.value,
+                    fill_f4=fill.value)
+
     def fallback_info(self):
         """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
         n = ctypes.c_int()

@@ -256,8 +256,15 @@ def run_reference(name, case):
             pr.prune(1)
         mine = prune_state_dict(sd_np, model_type, z=ex['prune'], group=4)
         pruned = {k: v.detach().numpy() for k, v in model.state_dict().items()}
+        n_cmp = 0
         for k in sd_np:
+            if pruned[k].dtype != np.float32:  # ('step' counter)
+                continue
             assert np.array_equal(pruned[k].view(np.uint32), np.asarray(mine[k], np.float32).view(np.uint32)), k
+            n_cmp += 1
+        from wavernn_amd.prune import block_density
+        print(f'{name}: reference Pruner masks == wavernn_amd.prune on {n_cmp} tensors; live 1x4 '
+              f'blocks {block_density(mine, model_type):.4f}', flush=True)
         sd_np = mine
     ref_sd = model.state_dict()
     new_sd = {}

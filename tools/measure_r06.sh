@@ -78,6 +78,18 @@ if [[ ,$S, == *,u10,* ]]; then
     run u10_nr$nr 300 env WRNN_PERSIST_NR_MAX=$nr WRNN_PERSIST_WIDE=0 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 $U10
   done
 fi
+# pruned checkpoints: the sparse GPU tests, then 90 %-pruned bench lines at C2
+# and at the 8-utterance shape, each beside the dense kernels on the same pruned weights
+[[ ,$S, == *,sparse,* ]] && run sparse 600 $PT tests/test_gpu_sparse.py
+if [[ ,$S, == *,sp,* ]]; then
+  run sp_c2 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --prune 0.9
+  run sp_c2_dense 300 env WRNN_SPARSE=0 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --prune 0.9
+  run sp_c4 400 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9 --utts-per-gpu 8
+  run sp_c4_dense 400 env WRNN_SPARSE=0 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9 --utts-per-gpu 8
+  for nr in 1 2 3 4; do
+    run sp_nr$nr 300 env WRNN_PERSIST_NR_MAX=$nr WRNN_PERSIST_ROT=0 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9
+  done
+fi
 [[ ,$S, == *,rehearse,* ]] && run rehearse 400 env WRNN_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --cpu-seconds 10
 [[ ,$S, == *,phase,* ]] && run phase 200 env WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0
 if [[ ,$S, == *,prof,* ]]; then
