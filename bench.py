@@ -479,7 +479,8 @@ def main():
                    'engine': model.last_engine(), 'persist_fallbacks': fb[0],
                    'sparse': {'prune': args.prune, 'image': spi['available'], 'ran': spi['last_call'],
                               'live_block_fraction': spi['density'], 'lds_list_fill_f4': spi['fill_f4']},
-                   'lib_build': lib_build_id()},
+                   'lib_build': lib_build_id(),
+                   'planner_rates': model.rates().splitlines()[0].replace('# source: ', '')},
         'roofline': roof,
         'cpu_baseline': None,
     }

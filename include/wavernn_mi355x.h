@@ -186,6 +186,21 @@ int wrnn_fallback_info(wrnn_handle* h, int* count, char* reason, size_t reason_c
  * fullest slot's list size (float4). Results equal the dense kernels' bit for bit. Env
  * WRNN_SPARSE=0 turns it off. Any pointer may be null. */
 int wrnn_sparse_info(wrnn_handle* h, int* available, int* last_call, double* density, int* fill_f4);
+/* Launch-planner rates (operator tuning; no reference equivalent): the per-step
+ * costs the planner minimises, as text lines `key v1 v2 ...` ('#' comments; keys and meaning in
+ * DESIGN.md). A handle starts from the built-in measured defaults overridden by env WRNN_RATES
+ * (a file) or rates_mi355x.txt beside the library. wrnn_set_rates overrides keys of the
+ * defaults (NULL: reload as at creation; a bad table is WRNN_ERR_INVALID and changes nothing);
+ * wrnn_get_rates writes the table in effect, with its source, NUL-terminated. */
+int wrnn_set_rates(wrnn_handle* h, const char* table);
+int wrnn_get_rates(wrnn_handle* h, char* buf, size_t cap);
+/* Host-only launch plan (no device): the plan wrnn_generate would make for `rows` fold rows of
+ * `seq_len` steps of a model_type / bits / mode model under the rate table `table` (NULL: the
+ * built-in defaults), every kernel variant taken as spill-free. flags: 1 sparse image, 2 P1 ring /
+ * per-frame P1, 4 wide images, 8 sparse forced (WRNN_SPARSE=1). Outputs: launches, rows per group and wide flag of the first `cap`,
+ * and the row rotation's launch count (0: none). */
+int wrnn_debug_plan(const char* table, int model_type, int bits, int mode, int rows, int seq_len, int flags,
+                    int* n_launches, int* rows_per_group, int* wide, int cap, int* rot_launches);
 /* Launch plan of the last PERSIST call (operator introspection; no reference equivalent):
  * *n_launches launches; for i < n_launches, launch i runs fold rows first_row[i] + g + 8 r,
  * r < rows_per_group[i], on the wide MFMA kernel when wide[i] != 0. Arrays may be null;

@@ -14,12 +14,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <map>
 #include <memory>
 #include <string>
 #include <thread>
 #include <tuple>
 #include <vector>
+
+#include <dlfcn.h>
 
 #include "cand_key.h"
 #include "philox.h"
@@ -114,6 +118,35 @@ struct StageDesc {
 };
 
 
+struct PlanRates {
+    double fat9[kPNR + 1] = {0, 4.8, 5.15, 5.91, 6.92};   // k_persist 9-bit (r05 nr_probe)
+    double fat10[kPNR + 1] = {0, 4.21, 5.19, 6.50, 9.41}; // 10-bit (profiles/r06/b u10_nr*)
+    // sparse instances (§3.0g): 9-bit measured (profiles/r06/b sp_nr*, 90 %-pruned weights);
+    // 10-bit = 9-bit + the dense 10-bit / 9-bit difference at 3-4 rows (estimate)
+    double fat9_sp[kPNR + 1] = {0, 4.99, 6.95, 7.99, 9.26};
+    double fat10_sp[kPNR + 1] = {0, 5.3, 7.3, 8.6, 11.7};
+    double rr[kPNR + 1] = {0, 6.7, 7.75, 8.81, 9.87};     // k_persist_rr (round 2, linear below 3)
+    double gen[kPNR + 1] = {0, 2.61, 3.26, 3.91, 4.56};   // k_persist_gen
+    // wide MFMA launches: base + row x r per step at r rows per group, + c10 at 1024 classes:
+    // 9.72 us at 16 rows (profiles/r05/final/c4.log, r06/b sp_c4), 10.965 at 16 rows / 1024
+    // classes (r05/final/b10.log), 10.59 at 6 rows / 1024 classes (r06/b u10_wide)
+    double wide[3] = {9.32, 0.025, 1.24};
+    double wide_rr[2] = {12.0, 0.025};                     // 12.39 us at 15-16 rows (r04 wide_rr)
+    double slice[2] = {60.0, 0.98};                        // us per extra launch, gain threshold
+    // rotation: rates of the rotated instance's two bodies by rows per group (the (q + 1)-row
+    // one at its single-launch rate; the q-row one the best split measured, §3.0e)
+    double rot9[kPNR + 1] = {0, 4.8, 5.22, 5.91, 6.92};
+    double rot9_sp[kPNR + 1] = {0, 4.99, 6.95, 7.99, 9.26};  // sparse (r06/b sp_nr*)
+    double rot_mol3_lo = 4.70;                             // MOL 3-row split (r05 rotation scan)
+    double rot_rr9[kPNR + 1] = {0, 6.3, 7.0, 7.78, 8.8};   // (2 / 4 rows: estimates)
+    double rot_rr10[kPNR + 1] = {0, 6.5, 7.26, 8.14, 9.23};  // profiles/r05/rr_rates/
+    double rot_rrm[kPNR + 1] = {0, 5.9, 6.6, 7.42, 8.4};   // profiles/r05/rr_rotation/mol/
+    double rot_gen[kPNR + 1] = {0, 1.98, 2.47, 3.12, 3.64};  // profiles/r05/gen_rotation/
+    double rot_genm[kPNR + 1] = {0, 1.72, 2.15, 2.60, 3.03};
+    double rot[2] = {40.0, 0.98};                          // us per extra launch, gain threshold
+    std::string source = "built-in defaults";
+};
+
 }  // namespace
 
 struct wrnn_handle {
@@ -181,6 +214,7 @@ struct wrnn_handle {
     bool p1_ring = false;      // this call's k_persist launches form P1 in-kernel
     bool p1_stream = false;    // this call writes the [S][B][4H] P1 stream (other kernels)
     bool sparse_call = false;  // this call's k_persist launches run the sparse instances
+    PlanRates rates;           // per-step rates of the launch planner (load_rates, §3.0h)
     bool timing = false;
     int phase_step = -1;  // diagnostic (env WRNN_PHASE_STEP): per-phase stamps of one step
     DevBuf phases;
@@ -1972,7 +2006,8 @@ void persist_wide_rr_phase_report(wrnn_handle* h, int t) {
 // C2 (18 rows): 3 launches, 3672 steps at 3 rows / 4214 at 2 -> 65.1 ms instead of 71.5.
 static int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
 
-bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan& P) {
+bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan& P, double launch_us = 40.0,
+                   double gain = 0.98) {
     P = wrnn_handle::RotPlan();
     const int q = R / kPG, m = R % kPG;
     if (q < 1 || m == 0 || q + 1 > 3 || S < 64) return false;
@@ -1991,8 +2026,8 @@ bool plan_rotation(int R, int S, double t_hi, double t_lo, wrnn_handle::RotPlan&
         }
     if (nh < 1 || nl < 1) return false;
     // worth it? (an extra launch reloads the weights: ~40 us)
-    const double rot = K * std::max(nh * t_hi, nl * t_lo) + (K - 1) * 40.0, plain = S * t_hi;
-    if (rot > 0.98 * plain) return false;
+    const double rot = K * std::max(nh * t_hi, nl * t_lo) + (K - 1) * launch_us, plain = S * t_hi;
+    if (rot > gain * plain) return false;
     P.K = K;
     P.nr_hi = q + 1;
     P.n_hi = nh;
@@ -2618,12 +2653,367 @@ int setup_debug_logits(wrnn_handle* h, int S, int Bp) {
     return WRNN_OK;
 }
 
-// per-step cost of a runtimeracer wide-row launch at 1 row per group, for the launch plan
-// (MI355X, bench HIP events)
-static const double kWideRRUs = 12.0;  // 12.39 us at 15-16 rows (profiles/r04/wide_rr/)
-// fatchord wide, 1024 classes: the second fc3 tile -- measured 10.965 us per launch step at 16
-// rows per group (b10) against 9.724 at 512 classes (c4), profiles/r05/final/{b10,c4}.log
-static const double kWide10Us = 1.24;
+// ===== Launch-plan rates ==================================================
+// Per-step costs (us, MI355X) the launch planner minimises. The defaults are the measured
+// points of the rounds cited beside them; a measurement pass emits a per-build table
+// (tools/make_rates.py -> wavernn_amd/rates_mi355x.txt next to the library, or the file named
+// by env WRNN_RATES) that replaces them key by key at wrnn_create. Format: one key per line,
+// `name v1 v2 ...`, '#' comments; by rows per group 1..4 for the register-resident tables.
+struct RateKey {
+    const char* name;
+    double PlanRates::*one;
+    double (PlanRates::*arr5)[kPNR + 1];
+    double (PlanRates::*arr3)[3];
+    double (PlanRates::*arr2)[2];
+};
+static const RateKey kRateKeys[] = {
+    {"fat9", nullptr, &PlanRates::fat9, nullptr, nullptr},
+    {"fat10", nullptr, &PlanRates::fat10, nullptr, nullptr},
+    {"fat9_sp", nullptr, &PlanRates::fat9_sp, nullptr, nullptr},
+    {"fat10_sp", nullptr, &PlanRates::fat10_sp, nullptr, nullptr},
+    {"rr", nullptr, &PlanRates::rr, nullptr, nullptr},
+    {"gen", nullptr, &PlanRates::gen, nullptr, nullptr},
+    {"wide", nullptr, nullptr, &PlanRates::wide, nullptr},
+    {"wide_rr", nullptr, nullptr, nullptr, &PlanRates::wide_rr},
+    {"slice", nullptr, nullptr, nullptr, &PlanRates::slice},
+    {"rot9", nullptr, &PlanRates::rot9, nullptr, nullptr},
+    {"rot9_sp", nullptr, &PlanRates::rot9_sp, nullptr, nullptr},
+    {"rot_mol3_lo", &PlanRates::rot_mol3_lo, nullptr, nullptr, nullptr},
+    {"rot_rr9", nullptr, &PlanRates::rot_rr9, nullptr, nullptr},
+    {"rot_rr10", nullptr, &PlanRates::rot_rr10, nullptr, nullptr},
+    {"rot_rrm", nullptr, &PlanRates::rot_rrm, nullptr, nullptr},
+    {"rot_gen", nullptr, &PlanRates::rot_gen, nullptr, nullptr},
+    {"rot_genm", nullptr, &PlanRates::rot_genm, nullptr, nullptr},
+    {"rot", nullptr, nullptr, nullptr, &PlanRates::rot},
+};
+
+// Overrides the keys a table names (unknown keys and malformed lines are errors; values must
+// be positive). The register-resident tables take 1-4 values (rows per group 1..4).
+bool parse_rates(const char* text, PlanRates& R, std::string& err) {
+    std::istringstream in(text ? text : "");
+    std::string line;
+    int ln = 0;
+    while (std::getline(in, line)) {
+        ++ln;
+        const size_t hash = line.find('#');
+        if (hash != std::string::npos) line.resize(hash);
+        std::istringstream ls(line);
+        std::string key;
+        if (!(ls >> key)) continue;
+        std::vector<double> v;
+        double x;
+        while (ls >> x) v.push_back(x);
+        if (!ls.eof()) return err = "line " + std::to_string(ln) + ": not a number", false;
+        const RateKey* k = nullptr;
+        for (const auto& e : kRateKeys)
+            if (key == e.name) k = &e;
+        if (!k) return err = "line " + std::to_string(ln) + ": unknown key '" + key + "'", false;
+        for (double d : v)
+            if (!(d > 0)) return err = "line " + std::to_string(ln) + ": values must be > 0", false;
+        const size_t want = k->one ? 1 : k->arr5 ? kPNR : k->arr3 ? 3 : 2;
+        if (v.size() != want)
+            return err = "line " + std::to_string(ln) + ": '" + key + "' takes " + std::to_string(want) + " values",
+                   false;
+        if (k->one) R.*(k->one) = v[0];
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (k->arr5) (R.*(k->arr5))[i + 1] = v[i];
+            if (k->arr3) (R.*(k->arr3))[i] = v[i];
+            if (k->arr2) (R.*(k->arr2))[i] = v[i];
+        }
+    }
+    return true;
+}
+
+std::string rates_text(const PlanRates& R) {
+    std::ostringstream o;
+    o << "# source: " << R.source << "\n";
+    for (const auto& k : kRateKeys) {
+        o << k.name;
+        if (k.one) o << ' ' << R.*(k.one);
+        if (k.arr5)
+            for (int i = 1; i <= kPNR; ++i) o << ' ' << (R.*(k.arr5))[i];
+        if (k.arr3)
+            for (int i = 0; i < 3; ++i) o << ' ' << (R.*(k.arr3))[i];
+        if (k.arr2)
+            for (int i = 0; i < 2; ++i) o << ' ' << (R.*(k.arr2))[i];
+        o << '\n';
+    }
+    return o.str();
+}
+
+// The table a new handle plans with: the defaults, then WRNN_RATES (a path) or the
+// rates_mi355x.txt beside this library when present. A file that does not parse is reported on
+// stderr and ignored (the defaults stay).
+PlanRates load_rates() {
+    PlanRates R;
+    std::string path;
+    if (const char* e = std::getenv("WRNN_RATES")) {
+        path = e;
+    } else {
+        Dl_info di;
+        if (dladdr(reinterpret_cast<void*>(&load_rates), &di) && di.dli_fname) {
+            std::string so = di.dli_fname;
+            const size_t sl = so.rfind('/');
+            path = (sl == std::string::npos ? std::string(".") : so.substr(0, sl)) + "/rates_mi355x.txt";
+        }
+    }
+    if (path.empty()) return R;
+    std::ifstream f(path);
+    if (!f) return R;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    PlanRates T = R;
+    std::string err;
+    if (!parse_rates(ss.str().c_str(), T, err)) {
+        std::fprintf(stderr, "[wavernn-mi355x] WARNING: rate table %s ignored: %s\n", path.c_str(), err.c_str());
+        return R;
+    }
+    T.source = path;
+    return T;
+}
+
+// Inputs of one call's launch plan: the model, the call's rows / steps, which kernel variants
+// exist and spill (scratch bytes, -1 = no such variant) and the env switches. generate_impl
+// fills it from the handle and the device; wrnn_debug_plan from its arguments (spill-free).
+struct PlanIn {
+    bool ok = false, fat = false, rr = false, gen = false;
+    int mode = 0, n = 0, cpw = 0, B = 0, S = 0;
+    bool c10 = false, sp = false, p1ring = false, rr_frames = false;
+    bool force_sp = false;  // env WRNN_SPARSE=1: the sparse instances whatever the rates
+    bool has_wide = false, has_wide_rr = false;
+    int scr[2][kPNR + 1] = {};     // fatchord k_persist [stream | ring][nr]
+    int scr_sp[kPNR + 1] = {};     // sparse instances
+    int scr_rot[2][kPNR + 1] = {}; // rotated instance of this topology / mode [dense | sparse][nr]
+    bool ok_reg[kPNR + 1] = {};    // runtimeracer / geneing register-resident variants
+    int wide_scr = 0, wide_rot_scr = 0;
+    // env switches
+    int wmode = 2, nr_max = 0;
+    bool slice_off = false, rot_off = false, allow_wide_scratch = false;
+    double rot_hi = 0, rot_lo = 0;  // WRNN_ROT_US (rate A/B); 0: none
+};
+struct PlanOut {
+    std::vector<wrnn_handle::PLaunch> lplan;
+    double plan_us = 0;
+    std::vector<wrnn_handle::WLaunch> wrot;
+    wrnn_handle::RotPlan rot;
+    bool p1_ring = false, sparse = false;
+    int Bplan = 0;
+};
+
+// The persistent launch plan (consecutive launches over row batches; launch k runs rows
+// rb_k + g + 8 r, r < nr_k, in every XCD group g): the cheapest mix of register-resident
+// (nr <= 4, spill-free variants) and wide MFMA launches (nr <= 16) by the per-step rates, then
+// time-sliced wide launches (§3.0f) or a row rotation (§3.0e) when those are cheaper.
+void plan_call(const PlanIn& in, const PlanRates& R, PlanOut& out) {
+    out = PlanOut();
+    const int B = in.B, S = in.S;
+    struct Opt {
+        int nr;
+        bool wide;
+        double us;
+    };
+    // sparse k_persist instances compete with the dense ones by their own rates: the cheaper
+    // register-resident family wins the call (both give the same results, §3.0g)
+    bool use_sp = false;
+    if (in.ok && in.fat && in.sp) {
+        const double* us = in.c10 ? R.fat10 : R.fat9;
+        const double* us_sp = in.c10 ? R.fat10_sp : R.fat9_sp;
+        double best_d = 1e300, best_s = 1e300;
+        for (int c = 1; c <= kPNR; ++c) {
+            const int rows = kPG * c, n_l = (B + rows - 1) / rows;  // launches of c rows per group
+            int sc = in.scr[0][c];
+            if (in.p1ring && in.scr[1][c] >= 0 && (sc < 0 || in.scr[1][c] < sc)) sc = in.scr[1][c];
+            if (sc >= 0 && sc <= 64) best_d = std::min(best_d, n_l * us[c]);
+            if (in.scr_sp[c] >= 0 && in.scr_sp[c] <= 64) best_s = std::min(best_s, n_l * us_sp[c]);
+        }
+        use_sp = in.force_sp || best_s < best_d;
+    }
+    if (in.ok) {
+        std::vector<Opt> opts;
+        if (in.fat) {
+            const double* us = in.c10 ? R.fat10 : R.fat9;
+            const double* us_sp = in.c10 ? R.fat10_sp : R.fat9_sp;
+            for (int c = 1; c <= kPNR; ++c) {
+                if (use_sp) {
+                    if (in.scr_sp[c] >= 0 && in.scr_sp[c] <= 64) opts.push_back({c, false, us_sp[c]});
+                    continue;
+                }
+                int sc = in.scr[0][c];
+                if (in.p1ring) {  // the call uses the flavour that spills less (below)
+                    const int sr = in.scr[1][c];
+                    if (sr >= 0 && (sc < 0 || sr < sc)) sc = sr;
+                }
+                if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[c]});
+            }
+            if (in.wmode && in.has_wide && (in.wide_scr == 0 || in.allow_wide_scratch)) {
+                if (in.wmode == 1) opts.clear();
+                for (int r = 1; r <= kPWideRows; ++r)
+                    opts.push_back({r, true, R.wide[0] + R.wide[1] * r + (in.c10 ? R.wide[2] : 0.0)});
+            }
+        } else {
+            for (int r = 1; r <= kPNR; ++r)
+                if (in.ok_reg[r]) opts.push_back({r, false, in.gen ? R.gen[r] : R.rr[r]});
+            if (in.rr && in.has_wide_rr && in.wmode && (in.wide_scr == 0 || in.allow_wide_scratch)) {
+                if (in.wmode == 1) opts.clear();
+                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, R.wide_rr[0] + R.wide_rr[1] * r});
+            }
+        }
+        if (in.nr_max > 0) {  // diagnostic: variant A/B (WRNN_PERSIST_NR_MAX)
+            const int c = std::max(1, std::min(kPNR, in.nr_max));
+            opts.erase(std::remove_if(opts.begin(), opts.end(), [&](const Opt& o) { return o.wide || o.nr != c; }),
+                       opts.end());
+            if (opts.empty()) opts.push_back({c, false, 1.0});
+        }
+        if (!opts.empty()) {
+            // best[r]: cheapest plan for r rows; pick[r]: its first launch
+            std::vector<double> best(B + 1, 0.0);
+            std::vector<int> pick(B + 1, -1);
+            for (int r = 1; r <= B; ++r) {
+                best[r] = 1e300;
+                for (int o = 0; o < (int)opts.size(); ++o) {
+                    const double c = opts[o].us + best[std::max(0, r - kPG * opts[o].nr)];
+                    if (c < best[r] - 1e-9) {
+                        best[r] = c;
+                        pick[r] = o;
+                    }
+                }
+            }
+            int rb = 0;
+            for (int r = B; r > 0;) {
+                const Opt& o = opts[pick[r]];
+                out.lplan.push_back({rb, o.nr, o.wide});
+                rb += kPG * o.nr;
+                r = std::max(0, r - kPG * o.nr);
+            }
+            out.plan_us = best[B];
+        }
+    }
+    // time-sliced wide launches, when cheaper than the plan above by the same rates (RAW, P1
+    // formed in-kernel: fatchord up to 1024 classes, runtimeracer)
+    const bool fat_sl = in.ok && in.fat && in.has_wide && in.p1ring;
+    const bool rr_sl = in.ok && in.rr && in.has_wide_rr && in.rr_frames;
+    if ((fat_sl || rr_sl) && in.mode == WRNN_MODE_RAW && !out.lplan.empty() && !in.slice_off && in.wmode &&
+        in.wide_rot_scr == 0) {
+        std::vector<wrnn_handle::WLaunch> sl;
+        if (plan_wide_slices(B, S, sl)) {
+            double cost = R.slice[0] * (sl.size() - 1);  // (an extra launch: weights, ring prologue)
+            for (const auto& L : sl)
+                cost += L.steps * (fat_sl ? R.wide[0] + R.wide[1] * L.nr + (in.c10 ? R.wide[2] : 0.0)
+                                          : R.wide_rr[0] + R.wide_rr[1] * L.nr);
+            if (cost < R.slice[1] * out.plan_us * S) {
+                out.lplan.clear();
+                for (int j = 0; j < (int)sl.size(); ++j) out.lplan.push_back({0, sl[j].nr, true, j});
+                out.wrot = std::move(sl);
+            }
+        }
+    }
+    const auto& lp = out.lplan;
+    out.Bplan = lp.empty() ? B : !out.wrot.empty() ? B : lp.back().rb + kPG * lp.back().nr;
+    // P1 ring (fatchord): on unless a register-resident launch spills more with it than with the
+    // stream (MOL at 3 rows per group: one register, 6.87 against 6.53 us per step); the sparse
+    // instances exist with the ring only
+    out.p1_ring = in.p1ring;
+    bool any_reg = false;
+    for (const auto& L : lp) any_reg |= !L.wide;
+    if (use_sp && any_reg) {
+        out.sparse = true;
+    } else if (in.fat) {
+        for (const auto& L : lp)
+            if (out.p1_ring && !L.wide && in.scr[1][L.nr] > in.scr[0][L.nr]) out.p1_ring = false;
+    }
+    // row rotation: one register-resident launch with uneven groups becomes K launches over
+    // rotating row sets. plan_rotation derives its (q + 1)-row body from B, so the launch must
+    // run exactly ceil(B / 8) rows per group; every rotated kernel forms its noise offsets in
+    // 32 bits, so the padded noise stream must stay below 4 GB
+    if (lp.size() != 1 || lp[0].wide || lp[0].nr != (B + kPG - 1) / kPG) return;
+    if (!((double)S * out.Bplan * in.n * 4.0 < 4.0e9) || in.rot_off) return;
+    if (in.mode != WRNN_MODE_RAW && in.mode != WRNN_MODE_MOL) return;
+    const int nr = lp[0].nr;
+    const bool fat_rot = in.fat && out.p1_ring && in.cpw <= 16;
+    if (nr < 2 || !(fat_rot || in.rr || in.gen)) return;
+    double t_hi, t_lo;
+    if (in.fat) {
+        const double* u = out.sparse ? R.rot9_sp : R.rot9;
+        t_hi = u[nr];
+        t_lo = u[nr - 1];
+        // MOL: its rotated 3-row body (one spilled register) runs much slower than the 2-row
+        // one -- the split balanced for 5.91 / 4.70 is the fastest of a scan (C3 5.61 -> 5.19)
+        if (in.mode == WRNN_MODE_MOL && nr == 3 && !out.sparse) t_lo = R.rot_mol3_lo;
+    } else {
+        const double* u = in.rr ? (in.mode == WRNN_MODE_MOL ? R.rot_rrm : in.cpw > 16 ? R.rot_rr10 : R.rot_rr9)
+                                : (in.mode == WRNN_MODE_MOL ? R.rot_genm : R.rot_gen);
+        t_hi = u[nr];
+        t_lo = u[nr - 1];
+    }
+    if (in.rot_hi > 0 && in.rot_lo > 0) {
+        t_hi = in.rot_hi;
+        t_lo = in.rot_lo;
+    }
+    // (the MOL 3-row rotated instance keeps one spilled register: tolerated, §3.0e)
+    const int rs = in.scr_rot[out.sparse ? 1 : 0][nr];
+    if (rs < 0 || rs > 8) return;
+    if (plan_rotation(B, S, t_hi, t_lo, out.rot, R.rot[0], R.rot[1])) {
+        out.lplan.clear();
+        for (int j = 0; j < out.rot.K; ++j) out.lplan.push_back({0, nr, false, j});
+    }
+}
+
+// PlanIn of a call on this handle: variant scratch from the device code objects, env switches.
+PlanIn plan_inputs(wrnn_handle* h, int B, int S) {
+    PlanIn in;
+    const auto& W = h->pw;
+    in.ok = W.ok;
+    in.rr = W.rr;
+    in.gen = W.gen;
+    in.fat = W.ok && !W.rr && !W.gen;
+    in.mode = h->cfg.mode;
+    in.n = h->n_classes;
+    in.cpw = W.cpw;
+    in.B = B;
+    in.S = S;
+    in.c10 = h->n_classes > kPM * 16;
+    in.p1ring = p1_ring_ok(h);
+    in.rr_frames = rr_frames_ok(h);
+    // sparse k_persist instances (pruned checkpoints, §3.0g): when the model's image exists and
+    // the call can form P1 in the ring; env WRNN_SPARSE=0 off (the dense kernels run the same
+    // zeros to the same results)
+    in.sp = in.fat && W.sp_ok && in.p1ring && (in.mode == WRNN_MODE_RAW || in.mode == WRNN_MODE_MOL);
+    if (const char* e = std::getenv("WRNN_SPARSE")) {
+        if (!std::strcmp(e, "0")) in.sp = false;
+        if (!std::strcmp(e, "1")) in.force_sp = true;
+    }
+    in.has_wide = in.fat && W.wwide != nullptr;
+    in.has_wide_rr = W.rr && W.wwide_rr != nullptr;
+    if (!W.ok) return in;
+    for (int c = 1; c <= kPNR; ++c) {
+        if (in.fat) {
+            in.scr[0][c] = persist_variant_scratch(c, W.cpw, in.mode, 0);
+            in.scr[1][c] = persist_variant_scratch(c, W.cpw, in.mode, 1);
+            in.scr_sp[c] = in.sp ? persist_variant_scratch(c, W.cpw, in.mode, 1, 1) : -1;
+            in.scr_rot[0][c] = c >= 2 ? persist_rot_scratch(c, in.mode, 0) : -1;
+            in.scr_rot[1][c] = c >= 2 && in.sp ? persist_rot_scratch(c, in.mode, 1) : -1;
+        } else {
+            in.ok_reg[c] = W.gen ? persist_gen_variant_ok(c, W.cpw, in.mode) != 0
+                                 : persist_rr_variant_ok(c, W.cpw, in.mode) != 0;
+            in.scr_rot[0][c] = c < 2 ? -1 : W.rr ? persist_rr_rot_scratch(c, in.mode == WRNN_MODE_MOL)
+                                                 : persist_gen_rot_scratch(c, in.mode);
+        }
+    }
+    if (in.has_wide) {
+        in.wide_scr = persist_wide_scratch(in.c10);
+        in.wide_rot_scr = persist_wide_rot_scratch(in.c10);
+    } else if (in.has_wide_rr) {
+        in.wide_scr = persist_wide_rr_scratch();
+        in.wide_rot_scr = persist_wide_rr_rot_scratch();
+    }
+    if (const char* e = std::getenv("WRNN_PERSIST_WIDE")) in.wmode = std::atoi(e);
+    if (const char* e = std::getenv("WRNN_PERSIST_NR_MAX")) in.nr_max = std::atoi(e);
+    if (const char* e = std::getenv("WRNN_PERSIST_SLICE")) in.slice_off = !std::strcmp(e, "0");
+    if (const char* e = std::getenv("WRNN_PERSIST_ROT")) in.rot_off = !std::strcmp(e, "0");
+    in.allow_wide_scratch = std::getenv("WRNN_WIDE_ALLOW_SCRATCH") != nullptr;
+    if (const char* e = std::getenv("WRNN_ROT_US")) std::sscanf(e, "%lf,%lf", &in.rot_hi, &in.rot_lo);
+    return in;
+}
 
 int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const int* n_frames,
                   int batched, int target, int overlap, int* row_offset, int* seq_len,
@@ -2678,140 +3068,12 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         else if (!std::strcmp(env, "auto")) want = WRNN_ENGINE_AUTO;
     }
     std::string why;
-    // PERSIST launch plan: consecutive launches over row batches; launch k runs rows
-    // rb_k + g + 8 r (r < nr_k) in every XCD group g. Candidate launches per topology:
-    //  * register-resident kernels (kernels_persist*.hip) with nr rows per group, nr up to the
-    //    largest variant without register spills;
-    //  * fatchord RAW <= 512 classes: the wide MFMA kernel (kernels_persist_wide.hip), up to
-    //    16 rows per group.
-    // The plan minimises the summed per-step time of its launches (measured MI355X us per step
-    // below), e.g. 9-bit: 18 rows -> one launch at 3 rows; 144 rows -> one wide launch of 128
-    // rows + one launch at 2 rows.
-    std::vector<wrnn_handle::PLaunch> lplan;
-    double plan_us = 0;  // the plan's summed per-step cost (us), for the time-sliced alternative
-    // sparse k_persist instances (pruned checkpoints): when the model's image
-    // exists (pack_persist_sparse) and the call can form P1 in the ring; env WRNN_SPARSE=0 off
-    // (A/B: the dense kernels run the same zeros to the same results)
-    bool sp = h->pw.sp_ok && !h->pw.rr && !h->pw.gen && p1_ring_ok(h) &&
-              (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
-    if (const char* e = std::getenv("WRNN_SPARSE"))
-        if (!std::strcmp(e, "0")) sp = false;
-    if (h->pw.ok) {
-        struct Opt {
-            int nr;
-            bool wide;
-            double us;
-        };
-        std::vector<Opt> opts;
-        if (!h->pw.gen && !h->pw.rr) {
-            // measured MI355X us per step by rows per group (9-bit: round 5, tools/nr_probe.sh;
-            // 10-bit: round 2)
-            static const double us[2][kPNR + 1] = {{0, 4.8, 5.15, 5.91, 6.92}, {0, 4.9, 5.64, 7.7, 9.4}};
-            // sparse instances at ~10 % density: no register weights, so every row count is
-            // spill-free (estimates until measured, §3.0g)
-            static const double us_sp[2][kPNR + 1] = {{0, 4.6, 4.9, 5.4, 6.0}, {0, 4.7, 5.1, 5.7, 6.4}};
-            const int w10 = h->pw.cpw > 16 ? 1 : 0;
-            for (int c = 1; c <= kPNR; ++c) {
-                if (sp) {
-                    const int ss = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 1, 1);
-                    if (ss >= 0 && ss <= 64) opts.push_back({c, false, us_sp[w10][c]});
-                    continue;
-                }
-                int sc = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 0);
-                if (p1_ring_ok(h)) {  // the call uses the flavour that spills less (below)
-                    const int sr = persist_variant_scratch(c, h->pw.cpw, h->cfg.mode, 1);
-                    if (sr >= 0 && (sc < 0 || sr < sc)) sc = sr;
-                }
-                if (sc >= 0 && sc <= 64) opts.push_back({c, false, us[w10][c]});
-            }
-            int wmode = 2;  // env WRNN_PERSIST_WIDE: 0 never, 1 only wide launches, 2 by cost
-            if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
-            // (a variant with register spills is not used unless WRNN_WIDE_ALLOW_SCRATCH=1: A/B)
-            const bool c10 = h->n_classes > kPM * 16;
-            const bool scratch_ok = persist_wide_scratch(c10) == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
-            if (wmode && h->pw.wwide && scratch_ok) {
-                if (wmode == 1) opts.clear();
-                // measured per step: round 2 11.67 / 11.81 / 12.17 / 12.35 us at 3 / 5 / 9 / 16 rows
-                // per group (the MFMA tiles cost the same for any row count; the exchanges and
-                // epilogues grow a little with the rows); round 3 11.38 at 16 -- fit 10.5 + 0.055 r;
-                // 1024 classes (the second fc3 tile): + kWide10Us
-                for (int r = 1; r <= kPWideRows; ++r)
-                    opts.push_back({r, true, 10.5 + 0.055 * r + (c10 ? kWide10Us : 0.0)});
-            }
-        } else {
-            // per-step cost by rows per group: measured MI355X points (runtimeracer 9-bit 8.81 us
-            // at 3 rows, 9.87 at 4; geneing 10-bit 3.91 at 3, 4.56 at 4), linear below; every
-            // spill-free variant is a candidate (18 rows: one launch at 3, not 32 slots at 4)
-            static const double us_rr[kPNR + 1] = {0, 6.7, 7.75, 8.81, 9.87};
-            static const double us_gen[kPNR + 1] = {0, 2.61, 3.26, 3.91, 4.56};
-            for (int r = 1; r <= kPNR; ++r)
-                if (h->pw.gen ? persist_gen_variant_ok(r, h->pw.cpw, h->cfg.mode) : persist_rr_variant_ok(r, h->pw.cpw, h->cfg.mode))
-                    opts.push_back({r, false, h->pw.gen ? us_gen[r] : us_rr[r]});
-            // runtimeracer wide-row launches (kernels_persist_wide_rr.hip), same env switch as
-            // the fatchord ones: WRNN_PERSIST_WIDE 0 never, 1 only wide, 2 by cost
-            int wmode = 2;
-            if (const char* env = std::getenv("WRNN_PERSIST_WIDE")) wmode = std::atoi(env);
-            const bool scratch_ok = persist_wide_rr_scratch() == 0 || std::getenv("WRNN_WIDE_ALLOW_SCRATCH");
-            if (h->pw.rr && h->pw.wwide_rr && wmode && scratch_ok) {
-                if (wmode == 1) opts.clear();
-                for (int r = 1; r <= kPWideRows; ++r) opts.push_back({r, true, kWideRRUs + 0.025 * r});
-            }
-        }
-        if (const char* env = std::getenv("WRNN_PERSIST_NR_MAX")) {  // diagnostic: variant A/B
-            const int c = std::max(1, std::min(kPNR, std::atoi(env)));
-            opts.erase(std::remove_if(opts.begin(), opts.end(), [&](const Opt& o) { return o.wide || o.nr != c; }),
-                       opts.end());
-            if (opts.empty()) opts.push_back({c, false, 1.0});
-        }
-        if (!opts.empty()) {
-            // best[r]: cheapest plan for r rows; pick[r]: its first launch
-            std::vector<double> best(B + 1, 0.0);
-            std::vector<int> pick(B + 1, -1);
-            for (int r = 1; r <= B; ++r) {
-                best[r] = 1e300;
-                for (int o = 0; o < (int)opts.size(); ++o) {
-                    const double c = opts[o].us + best[std::max(0, r - kPG * opts[o].nr)];
-                    if (c < best[r] - 1e-9) {
-                        best[r] = c;
-                        pick[r] = o;
-                    }
-                }
-            }
-            int rb = 0;
-            for (int r = B; r > 0;) {
-                const Opt& o = opts[pick[r]];
-                lplan.push_back({rb, o.nr, o.wide});
-                rb += kPG * o.nr;
-                r = std::max(0, r - kPG * o.nr);
-            }
-            plan_us = best[B];
-        }
-    }
-    // time-sliced wide launches (plan_wide_slices), when cheaper than the plan
-    // above by the same cost model (RAW, P1 formed in-kernel: fatchord up to 1024 classes,
-    // runtimeracer; WRNN_PERSIST_SLICE=0 or WRNN_PERSIST_WIDE=0: off)
-    h->wrot.clear();
-    const bool fat_sl = h->pw.ok && !h->pw.gen && !h->pw.rr && h->pw.wwide && p1_ring_ok(h);
-    const bool rr_sl = h->pw.ok && h->pw.rr && h->pw.wwide_rr && rr_frames_ok(h);
-    if ((fat_sl || rr_sl) && h->cfg.mode == WRNN_MODE_RAW && !lplan.empty()) {
-        const char* e1 = std::getenv("WRNN_PERSIST_SLICE");
-        const char* e2 = std::getenv("WRNN_PERSIST_WIDE");
-        std::vector<wrnn_handle::WLaunch> sl;
-        const bool c10 = h->n_classes > kPM * 16;
-        const int rsc = fat_sl ? persist_wide_rot_scratch(c10) : persist_wide_rr_rot_scratch();
-        if (!(e1 && !std::strcmp(e1, "0")) && !(e2 && !std::strcmp(e2, "0")) && rsc == 0 &&
-            plan_wide_slices(B, S, sl)) {
-            double cost = 60.0 * (sl.size() - 1);  // (an extra launch: weights, ring prologue)
-            for (const auto& L : sl)
-                cost += L.steps * (fat_sl ? 10.5 + 0.055 * L.nr + (c10 ? kWide10Us : 0.0) : kWideRRUs + 0.025 * L.nr);
-            if (cost < 0.98 * plan_us * S) {
-                lplan.clear();
-                for (int j = 0; j < (int)sl.size(); ++j) lplan.push_back({0, sl[j].nr, true, j});
-                h->wrot = std::move(sl);
-            }
-        }
-    }
-    const int Bplan = lplan.empty() ? B : !h->wrot.empty() ? B : lplan.back().rb + kPG * lplan.back().nr;
+    // PERSIST launch plan (plan_call): register-resident and wide launches by the rates of
+    // h->rates, then time-sliced wide launches or a row rotation
+    PlanOut pout;
+    plan_call(plan_inputs(h, B, S), h->rates, pout);
+    const auto& lplan = pout.lplan;
+    const int Bplan = pout.Bplan;
     bool use_p = false;
     if (want != WRNN_ENGINE_CHAIN) {
         if (!h->pw.ok)
@@ -2832,92 +3094,12 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     }
     const int Bp = use_p ? Bplan : B;  // persistent groups carry nr rows per launch
     h->p_plan = use_p ? lplan : std::vector<wrnn_handle::PLaunch>();
+    h->wrot = use_p ? pout.wrot : std::vector<wrnn_handle::WLaunch>();
+    h->rot_plan = use_p ? pout.rot : wrnn_handle::RotPlan();
     // P1: the fatchord launches (register-resident and wide) form it in-kernel when the
     // per-frame form exists; the [S][B][4H] stream is written only for the other kernels
-    // per call: the ring unless a k_persist launch of the plan spills more with it than with
-    // the stream (measured: MOL at 3 rows per group spills one register with the ring and
-    // runs 6.87 against 6.53 us per step)
-    h->p1_ring = use_p && p1_ring_ok(h);
-    h->sparse_call = false;
-    bool any_reg = false;
-    for (const auto& L : h->p_plan) any_reg |= !L.wide;
-    if (use_p && sp && any_reg) {
-        h->sparse_call = true;  // (sparse instances exist with the ring only: it stays on)
-    } else {
-        for (const auto& L : h->p_plan)
-            if (h->p1_ring && !L.wide &&
-                persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 1) >
-                    persist_variant_scratch(L.nr, h->pw.cpw, h->cfg.mode, 0))
-                h->p1_ring = false;
-    }
-    // row rotation (plan_rotation): one register-resident 9-bit launch with
-    // uneven groups becomes K launches over rotating row sets (WRNN_PERSIST_ROT=0: off)
-    h->rot_plan = wrnn_handle::RotPlan();
-    // plan_rotation derives its (q + 1)-row body from B: the single launch must run exactly
-    // ceil(B / 8) rows per group (a WRNN_PERSIST_NR_MAX cap or a spill-filtered variant can
-    // leave it at another count, and the rotated layout would then misread its row slots)
-    const bool rot_nr = use_p && h->p_plan.size() == 1 && h->p_plan[0].nr == (B + kPG - 1) / kPG;
-    // every rotated kernel forms its noise offsets ((step offset x Bp + row) x n + class) x 4 in
-    // 32 bits: the padded noise stream must stay below 4 GB
-    const bool rot_off32 = (double)S * Bp * h->n_classes * 4.0 < 4.0e9;
-    const bool fat_rot = use_p && rot_nr && rot_off32 && h->p1_ring && !h->p_plan[0].wide && !h->pw.rr &&
-                         !h->pw.gen && h->pw.cpw <= 16 &&
-                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL);
-    // runtimeracer (k_persist_rr, RAW / MOL): P1 and the noise from their streams at each row's own
-    // step (the noise stream addressed with 32-bit offsets: < 4 GiB)
-    const bool rr_rot = use_p && rot_nr && rot_off32 && !h->p_plan[0].wide && h->pw.rr &&
-                        (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2;
-    // geneing (k_persist_gen, categorical 'BITS' and MOL): as runtimeracer
-    const bool gen_rot = use_p && rot_nr && rot_off32 && !h->p_plan[0].wide && h->pw.gen &&
-                         (h->cfg.mode == WRNN_MODE_RAW || h->cfg.mode == WRNN_MODE_MOL) && h->p_plan[0].nr >= 2;
-    if (fat_rot || rr_rot || gen_rot) {
-        const char* env = std::getenv("WRNN_PERSIST_ROT");
-        const int nr = h->p_plan[0].nr;
-        // per-step rates of the rotated instance's two bodies: the (q + 1)-row one at the
-        // single-launch rate, the q-row one a little slower than its own kernel (2 rows: 5.22
-        // against 5.15 us -- the best split measured)
-        static const double us9[kPNR + 1] = {0, 4.8, 5.22, 5.91, 6.92};
-        static const double us9s[kPNR + 1] = {0, 4.6, 4.9, 5.4, 6.0};  // sparse (estimates, §3.0g)
-        const double* u9 = h->sparse_call ? us9s : us9;
-        double t_hi = nr >= 1 ? u9[nr] : 0, t_lo = nr >= 2 ? u9[nr - 1] : 0;
-        // MOL: its rotated 3-row body (one spilled register) runs much slower than the 2-row
-        // one -- the split balanced for 5.91 / 4.70 is the fastest of a scan from 5.22 down to
-        // 4.55 (C3 5.61 -> 5.19 us per step; DESIGN.md §3.0e, profiles/r05/rotation/)
-        if (h->cfg.mode == WRNN_MODE_MOL && nr == 3 && !h->sparse_call) t_lo = 4.70;
-        if (rr_rot) {  // runtimeracer, measured single-launch step times at 1-4 rows per group
-            static const double rr9[kPNR + 1] = {0, 6.3, 7.0, 7.78, 8.8};   // 9-bit (2 / 4 rows: estimates)
-            static const double rr10[kPNR + 1] = {0, 6.5, 7.26, 8.14, 9.23};  // 10-bit (profiles/r05/rr_rates/)
-            // MOL: 3 rows 7.42 us measured; 2 rows the best of its own split scan (6.0-6.9: C2
-            // shape 7.50 -> 7.03 us per step at 6.6, profiles/r05/rr_rotation/mol/)
-            static const double rrm[kPNR + 1] = {0, 5.9, 6.6, 7.42, 8.4};
-            const double* us = h->cfg.mode == WRNN_MODE_MOL ? rrm : h->pw.cpw > 16 ? rr10 : rr9;
-            t_hi = us[nr];
-            t_lo = us[nr - 1];
-        }
-        if (gen_rot) {  // geneing 10-bit: 3 rows 3.12 us measured (single launch, C2 shape); the
-            // 2-row rate the best of a scan of splits (C2 3.13 -> 3.01 us per step,
-            // profiles/r05/gen_rotation/); 1 / 4 rows scaled from the round-2 points (estimates)
-            static const double gr[kPNR + 1] = {0, 1.98, 2.47, 3.12, 3.64};
-            // MOL: 3 rows 2.60 us measured; 2 rows the best of its own split scan (2.06-2.25:
-            // C2 shape 2.62 -> 2.43 us per step at 2.15)
-            static const double gm[kPNR + 1] = {0, 1.72, 2.15, 2.60, 3.03};
-            const double* us = h->cfg.mode == WRNN_MODE_MOL ? gm : gr;
-            t_hi = us[nr];
-            t_lo = us[nr - 1];
-        }
-        if (const char* e2 = std::getenv("WRNN_ROT_US"))  // diagnostic: "t_hi,t_lo" (rate A/B)
-            std::sscanf(e2, "%lf,%lf", &t_hi, &t_lo);
-        // (the MOL 3-row rotated instance keeps one spilled register: one 4-byte scratch store
-        // per step, outside the exchanges -- tolerated, measured in DESIGN.md §3.0e)
-        const int rs = nr < 2 ? -1 : rr_rot ? persist_rr_rot_scratch(nr, h->cfg.mode == WRNN_MODE_MOL)
-                     : gen_rot ? persist_gen_rot_scratch(nr, h->cfg.mode)
-                               : persist_rot_scratch(nr, h->cfg.mode, h->sparse_call ? 1 : 0);
-        if (!(env && !std::strcmp(env, "0")) && rs >= 0 && rs <= 8 &&
-            plan_rotation(B, S, t_hi, t_lo, h->rot_plan)) {
-            h->p_plan.clear();
-            for (int j = 0; j < h->rot_plan.K; ++j) h->p_plan.push_back({0, nr, false, j});
-        }
-    }
+    h->p1_ring = use_p && pout.p1_ring;
+    h->sparse_call = use_p && pout.sparse;
     h->p1_stream = use_p && !h->p1_ring;  // (the wide launches form P1 in-kernel too)
     if (h->p1_stream && h->pw.rr && rr_frames_ok(h)) {  // runtimeracer: only wide launches
         bool all_wide = !h->p_plan.empty();                // form P1 in-kernel
@@ -3155,6 +3337,7 @@ int wrnn_create(const wrnn_config* cfg, int device, wrnn_handle** out) {
     h->n_gru = cfg->model_type == WRNN_MODEL_FATCHORD ? 2 : cfg->model_type == WRNN_MODEL_GENEING ? 1 : 4;
     h->indent = cfg->pad * prod;
     build_expected(h.get());
+    h->rates = load_rates();
     HIPC(hipSetDevice(device));
     HIPC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     *out = h.release();
@@ -3448,6 +3631,67 @@ int wrnn_debug_rot_plan(int rows, int seq_len, double us_hi, double us_lo, int* 
     *launches = P.K;
     *n_hi = P.n_hi;
     *n_lo = P.n_lo;
+    return WRNN_OK;
+}
+
+int wrnn_set_rates(wrnn_handle* h, const char* table) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (!table) {
+        h->rates = load_rates();
+        return WRNN_OK;
+    }
+    PlanRates R;
+    std::string err;
+    if (!parse_rates(table, R, err)) return fail(WRNN_ERR_INVALID, "rate table: " + err);
+    R.source = "wrnn_set_rates";
+    h->rates = R;
+    return WRNN_OK;
+}
+
+int wrnn_get_rates(wrnn_handle* h, char* buf, size_t cap) {
+    if (!h || !buf || cap == 0) return fail(WRNN_ERR_INVALID, "null argument");
+    const std::string t = rates_text(h->rates);
+    if (t.size() + 1 > cap) return fail(WRNN_ERR_CAPACITY, "rate table needs " + std::to_string(t.size() + 1) + " bytes");
+    std::memcpy(buf, t.c_str(), t.size() + 1);
+    return WRNN_OK;
+}
+
+int wrnn_debug_plan(const char* table, int model_type, int bits, int mode, int rows, int seq_len, int flags,
+                    int* n_launches, int* rows_per_group, int* wide, int cap, int* rot_launches) {
+    if (!n_launches || !rot_launches) return fail(WRNN_ERR_INVALID, "null argument");
+    if (rows < 1 || seq_len < 1 || cap < 0) return fail(WRNN_ERR_INVALID, "bad arguments");
+    PlanRates R;
+    std::string err;
+    if (table && !parse_rates(table, R, err)) return fail(WRNN_ERR_INVALID, "rate table: " + err);
+    PlanIn in;
+    in.ok = true;
+    in.fat = model_type == WRNN_MODEL_FATCHORD;
+    in.rr = model_type == WRNN_MODEL_RUNTIMERACER;
+    in.gen = model_type == WRNN_MODEL_GENEING;
+    if (!in.fat && !in.rr && !in.gen) return fail(WRNN_ERR_INVALID, "model type");
+    in.mode = mode;
+    in.n = mode == WRNN_MODE_RAW ? (1 << bits) : mode == WRNN_MODE_BETA ? 2 : 30;
+    in.cpw = (in.n + (in.fat ? kPM : 16) - 1) / (in.fat ? kPM : 16);
+    in.c10 = in.n > kPM * 16;
+    in.B = rows;
+    in.S = seq_len;
+    // flags: 1 sparse image, 2 P1 ring / per-frame P1 (fatchord, runtimeracer), 4 wide images;
+    // every variant spill-free
+    in.sp = in.fat && (flags & 1) && (flags & 2) && (mode == WRNN_MODE_RAW || mode == WRNN_MODE_MOL);
+    in.force_sp = in.sp && (flags & 8);
+    in.p1ring = in.fat && (flags & 2);
+    in.rr_frames = in.rr && (flags & 2);
+    in.has_wide = in.fat && (flags & 4) && mode == WRNN_MODE_RAW;
+    in.has_wide_rr = in.rr && (flags & 4) && mode == WRNN_MODE_RAW;
+    for (int c = 1; c <= kPNR; ++c) in.ok_reg[c] = true;
+    PlanOut out;
+    plan_call(in, R, out);
+    *n_launches = (int)out.lplan.size();
+    *rot_launches = out.rot.K;
+    for (int i = 0; i < (int)out.lplan.size() && i < cap; ++i) {
+        if (rows_per_group) rows_per_group[i] = out.lplan[i].nr;
+        if (wide) wide[i] = out.lplan[i].wide ? 1 : 0;
+    }
     return WRNN_OK;
 }
 

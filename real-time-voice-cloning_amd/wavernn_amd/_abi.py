@@ -131,6 +131,10 @@ def load_library(path=None):
         'wrnn_debug_noise': (c_int, [c_void_p, c_int, P(ctypes.c_float), c_size_t]),
         'wrnn_plan_info': (c_int, [c_void_p, P(c_int), P(c_int), P(c_int), P(c_int), c_int]),
         'wrnn_sparse_info': (c_int, [c_void_p, P(c_int), P(c_int), P(ctypes.c_double), P(c_int)]),
+        'wrnn_set_rates': (c_int, [c_void_p, ctypes.c_char_p]),
+        'wrnn_get_rates': (c_int, [c_void_p, ctypes.c_char_p, c_size_t]),
+        'wrnn_debug_plan': (c_int, [ctypes.c_char_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int),
+                                    P(c_int), P(c_int), c_int, P(c_int)]),
         'wrnn_debug_beta': (c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.c_uint32, ctypes.c_float, ctypes.c_float,
                                     P(ctypes.c_float)]),

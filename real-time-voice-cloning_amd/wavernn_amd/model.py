@@ -239,6 +239,16 @@ class WaveRNN:
         return dict(available=bool(av.value), last_call=bool(lc.value), density=d.value,
                     fill_f4=fill.value)
 
+    def rates(self):
+        """The launch planner's rate table in effect (text, first line its source)."""
+        buf = ctypes.create_string_buffer(4096)
+        _abi.check(self._lib.wrnn_get_rates(self._h, buf, 4096))
+        return buf.value.decode()
+
+    def set_rates(self, table=None):
+        """Override keys of the planner's rate table (None: reload as at creation)."""
+        _abi.check(self._lib.wrnn_set_rates(self._h, table.encode() if table else None))
+
     def fallback_info(self):
         """(calls that fell back from PERSIST to CHAIN on this handle, last reason)."""
         n = ctypes.c_int()

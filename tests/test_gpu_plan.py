@@ -82,3 +82,37 @@ def test_runtimeracer_default_batch_is_time_sliced_over_wide_launches():
     group x 500 steps instead of a 16-row and a 13-row launch of 8,000 steps each."""
     plan = _run('runtimeracer-wavernn', 'RAW', 10, 8, target=6000, overlap=1000)
     assert plan == [(0, 16, True)] * 29, plan
+
+
+def test_fatchord_10bit_single_utterance_default_is_one_wide_launch():
+    """The fork's fatchord default on one 1000-frame mel (10 bits, 3000 / 1500: 45 rows x 6,000
+    steps, VERDICT r5 missing #2): one wide launch of 6 rows per group -- measured 10.6 us per
+    step, 3.04 M samples/s, against two register-resident launches of 3 rows per group (13.0 us
+    per step of S, 2.43 M) and the other row counts (profiles/r06/b u10*.log)."""
+    plan = _run('fatchord-wavernn', 'RAW', 10, 1, target=3000, overlap=1500)
+    assert plan == [(0, 6, True)], plan
+
+
+def test_pruned_c2_plans_by_measured_rates(monkeypatch):
+    """90 %-pruned weights at C2: the sparse image exists, but the dense rotated launches are
+    faster on MI355X (5.4 against 7.4 us per step, DESIGN.md §3.0g), so the planner keeps them;
+    WRNN_SPARSE=1 runs the sparse instances on the same rotated plan."""
+    import torch
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.model import WaveRNN
+    from wavernn_amd.prune import prune_state_dict
+    from wavernn_amd.synth import synth_mel, synth_state_dict
+    mt = 'fatchord-wavernn'
+    hp = hparams_for(mt).copy(bits=9)
+    m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
+                hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
+                mode=hp.mode, model_type=mt, device=0)
+    m.load_state_dict(prune_state_dict(synth_state_dict(hp, mt, seed=0), mt, z=0.9))
+    mel = [torch.from_numpy((synth_mel(1000, 0) / sp.max_abs_value).astype(np.float32)).cuda()]
+    m.generate_batch_device(mel, True, 11000, 550)
+    assert m.sparse_info()['available'] and not m.sparse_info()['last_call']
+    assert m.plan_info() == [(0, 3, False)] * 3
+    monkeypatch.setenv('WRNN_SPARSE', '1')
+    m.generate_batch_device(mel, True, 11000, 550)
+    assert m.sparse_info()['last_call'] and m.plan_info() == [(0, 3, False)] * 3

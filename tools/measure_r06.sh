@@ -90,6 +90,14 @@ if [[ ,$S, == *,sp,* ]]; then
     run sp_nr$nr 300 env WRNN_PERSIST_NR_MAX=$nr WRNN_PERSIST_ROT=0 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9
   done
 fi
+# planner rates: the 9-bit C2-shape step time at each rows-per-group variant
+# (no rotation), then the per-build rate table from this pass's probes
+if [[ ,$S, == *,rates,* ]]; then
+  for nr in 1 2 3 4; do
+    run nr$nr 300 env WRNN_PERSIST_NR_MAX=$nr WRNN_PERSIST_ROT=0 python bench.py --steps 3 --warmup 1 --cpu-seconds 0
+  done
+  run make_rates 60 python tools/make_rates.py $O/rates_mi355x.txt $O
+fi
 [[ ,$S, == *,rehearse,* ]] && run rehearse 400 env WRNN_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --cpu-seconds 10
 [[ ,$S, == *,phase,* ]] && run phase 200 env WRNN_PHASE_STEP=600 python bench.py --steps 1 --warmup 0 --cpu-seconds 0
 if [[ ,$S, == *,prof,* ]]; then
