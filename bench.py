@@ -52,6 +52,9 @@ def parse():
                     help='prune the synthetic weights as the reference Pruner does at this '
                          'sparsity in 1x4 groups (vocoder/pruner.py; 0.9 = its target): the '
                          'block-sparse kernels run them (DESIGN.md §3.0g)')
+    ap.add_argument('--sparse', default='auto', choices=['auto', '0', '1'],
+                    help='block-sparse k_persist instances for pruned weights: by the planner '
+                         '(auto), never (0), always (1) -- env WRNN_SPARSE')
     ap.add_argument('--engine', default='auto', choices=['auto', 'chain', 'persist'],
                     help='recurrence engine (include/wavernn_mi355x.h WRNN_ENGINE_*)')
     return ap.parse_args()
@@ -267,6 +270,8 @@ def cpu_baseline(args, sd, hp, mel, gpu_rows, gpu_wav, seed, stream):
 
 def main():
     args = parse()
+    if args.sparse != 'auto':
+        os.environ['WRNN_SPARSE'] = args.sparse
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -429,7 +434,7 @@ def main():
                                      f'{nr} rows per XCD group')
         # HBM traffic of the same kernel on the same workload from the committed PMC passes
         # (rocprofv3 cannot run inside this process; profiles/pmc_traffic.json names its source)
-        pmc = _pmc_traffic(kernel, workload)
+        pmc = _pmc_traffic(kernel.replace(' (sparse)', ''), workload)
         if pmc:
             roof['traffic'] = pmc['traffic_bytes']
             roof['traffic_source'] = pmc['source']

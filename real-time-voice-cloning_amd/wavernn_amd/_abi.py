@@ -40,6 +40,7 @@ EXPORTED = [
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
     'wrnn_debug_beta', 'wrnn_debug_decide', 'wrnn_debug_rot_plan', 'wrnn_debug_slice_plan', 'wrnn_rot_info', 'wrnn_persist_steps', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
     'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits', 'wrnn_debug_wide_layout',
+    'wrnn_sparse_info', 'wrnn_set_rates', 'wrnn_get_rates', 'wrnn_debug_plan',
 ]
 
 

@@ -74,10 +74,14 @@ def kernels_of(lib):
 
 
 def dbg_pairs(kern):
-    """(production name, DBG name) pairs: the DBG flag is the last template argument."""
+    """(production name, DBG name) pairs: the DBG flag is the last template argument, except in
+    k_persist, whose last one is SP (the sparse instances, round 6): DBG is the one before it."""
     pairs = []
     for name in kern:
-        m = re.match(r'^(.*)Lb1E(EEvN.*)$', name)
+        if '9k_persistI' in name:
+            m = re.match(r'^(.*)Lb1E(Lb[01]EEEvN.*)$', name)
+        else:
+            m = re.match(r'^(.*)Lb1E(EEvN.*)$', name)
         if m and (m.group(1) + 'Lb0E' + m.group(2)) in kern:
             pairs.append((m.group(1) + 'Lb0E' + m.group(2), name))
     return pairs

@@ -40,12 +40,14 @@ if [[ ,$S, == *,pmc,* ]]; then
   python -c "import sys; sys.path[:0]=['.', 'real-time-voice-cloning_amd']; import bench; print(bench.lib_build_id())" > $P/lib_build
   B="/usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 --no-timing"
   SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
-  for m in ${PMC_SET:-c2 c4 rr b10 gen}; do
+  for m in ${PMC_SET:-c2 c4 rr b10 gen u10 spc2}; do
     A=""; K="k_persist<"
     [ $m = gen ] && A="--model geneing-wavernn --mode BITS --bits 10" && K="k_persist_gen<"
     [ $m = c4 ] && A="--utts-per-gpu 8" && K="k_persist_wide<"
     [ $m = rr ] && A="$RR" && K="k_persist_wide_rr"
     [ $m = b10 ] && A="$B10" && K="k_persist_wide<"
+    [ $m = u10 ] && A="--bits 10 --target 3000 --overlap 1500" && K="k_persist_wide<"
+    [ $m = spc2 ] && A="--prune 0.9 --sparse 1"
     run ${m}_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_fetch" -o run --output-format csv -- $B $A
     run ${m}_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d "$PWD/$P/${m}_write" -o run --output-format csv -- $B $A
     run ${m}_sq 240 rocprofv3 --pmc $SQ --kernel-include-regex "$K" -d "$PWD/$P/${m}_sq" -o run --output-format csv -- $B $A
@@ -105,5 +107,15 @@ if [[ ,$S, == *,prof,* ]]; then
   run prof_c4 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_c4" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --utts-per-gpu 8
   run prof_rr 400 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_rr" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 $RR
   run prof_b10 400 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_b10" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 $B10
+  run prof_u10 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_u10" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --bits 10 --target 3000 --overlap 1500
+  run prof_spc2 300 rocprofv3 --kernel-trace --stats -d "$PWD/$O/prof_spc2" -o run --output-format csv -- /usr/bin/python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9 --sparse 1
+fi
+# round-6 final lines: the fork's 10-bit single utterance, C2 on 90 %-pruned weights (planner's
+# choice = dense, and the sparse instances forced), the 8-utterance shape on pruned weights
+if [[ ,$S, == *,r6lines,* ]]; then
+  run u10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --bits 10 --target 3000 --overlap 1500
+  run spc2_auto 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --prune 0.9
+  run spc2 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 --prune 0.9 --sparse 1
+  run spc4 400 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --prune 0.9 --utts-per-gpu 8
 fi
 exit 0

@@ -32,9 +32,10 @@ CORR = ("FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE talli
 N_SIMD = 1024
 
 
-def workload(model, wname, frames=1000, utts=1, target=11000, overlap=550):
+def workload(model, wname, frames=1000, utts=1, target=11000, overlap=550, prune=0.0):
     return (f'{utts}x{frames}-frame mel per GPU, {model} {wname}, '
-            f'batched folds target={target} overlap={overlap}')
+            f'batched folds target={target} overlap={overlap}' +
+            (f', weights pruned {prune:.2f} in 1x4 blocks' if prune else ''))
 
 
 # workload -> (bench.py arguments as in tools/pmc_r03.sh ARGS, bench workload string, kernel)
@@ -50,6 +51,12 @@ WORKLOADS = {
            'k_persist_wide_rr'),
     'gen': (' --model geneing-wavernn --mode BITS --bits 10',
             workload('geneing-wavernn', 'BITS 10-bit'), 'k_persist_gen'),
+    # round 6: the fork's fatchord 10-bit single utterance (one wide launch of 6 rows per group)
+    # and C2 on 90 %-pruned weights with the sparse instances forced
+    'u10': (' --bits 10 --target 3000 --overlap 1500',
+            workload('fatchord-wavernn', 'RAW 10-bit mu-law', target=3000, overlap=1500), 'k_persist_wide'),
+    'spc2': (' --prune 0.9 --sparse 1', workload('fatchord-wavernn', 'RAW 9-bit mu-law', prune=0.9),
+             'k_persist'),
 }
 
 
