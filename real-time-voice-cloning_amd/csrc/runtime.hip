@@ -3671,7 +3671,7 @@ int wrnn_debug_plan(const char* table, int model_type, int bits, int mode, int r
     if (!in.fat && !in.rr && !in.gen) return fail(WRNN_ERR_INVALID, "model type");
     in.mode = mode;
     in.n = mode == WRNN_MODE_RAW ? (1 << bits) : mode == WRNN_MODE_BETA ? 2 : 30;
-    in.cpw = (in.n + (in.fat ? kPM : 16) - 1) / (in.fat ? kPM : 16);
+    in.cpw = (in.n + kPM - 1) / kPM;  // (classes per slot, as pack_persist* sets it)
     in.c10 = in.n > kPM * 16;
     in.B = rows;
     in.S = seq_len;
