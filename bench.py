@@ -434,7 +434,7 @@ def main():
                                      f'{nr} rows per XCD group')
         # HBM traffic of the same kernel on the same workload from the committed PMC passes
         # (rocprofv3 cannot run inside this process; profiles/pmc_traffic.json names its source)
-        pmc = _pmc_traffic(kernel.replace(' (sparse)', ''), workload)
+        pmc = _pmc_traffic(kernel, workload)
         if pmc:
             roof['traffic'] = pmc['traffic_bytes']
             roof['traffic_source'] = pmc['source']

@@ -1,13 +1,14 @@
 """Write <round dir>/summary.md from a tools/measure_r05.sh pass (bench lines, PMC fold, kernel stats).
 
-usage: python tools/final_summary.py <pass dir> <round dir> <tag>
+usage: python tools/final_summary.py <pass dir> <round dir> <tag> [<round name>]
 """
 import csv
 import json
 import os
 import sys
 
-LINES = ('bench', 'c4', 'rr', 'b10', 'c3', 'gen', 'gen_norot', 'gen_mol', 'rr_mol', 'rr9')
+LINES = ('bench', 'c4', 'rr', 'b10', 'c3', 'gen', 'gen_norot', 'gen_mol', 'rr_mol', 'rr9',
+         'u10', 'spc2_auto', 'spc2', 'spc4')
 
 
 def bench_line(path):
@@ -23,8 +24,9 @@ def main():
     src, out, tag = sys.argv[1:4]
     tests = open(os.path.join(src, 'tests.log')).read() if os.path.exists(os.path.join(src, 'tests.log')) else ''
     passed = [l for l in tests.splitlines() if ' passed' in l and '====' in l]
-    L = ['# Round-5 final measurement pass (MI355X)', '',
-         f'`tools/measure_r05.sh` (TAG={tag}) on the final library build; GPU tests `tests.log` '
+    rnd = sys.argv[4] if len(sys.argv) > 4 else 'Round-5'
+    L = [f'# {rnd} final measurement pass (MI355X)', '',
+         f'`tools/measure_r0{rnd[-1]}.sh` (TAG={tag}) on the final library build; GPU tests `tests.log` '
          f'({passed[-1].strip("= ") if passed else "see log"}), smoke `smoke.log`; counters `pmc/` (folded into '
          '`profiles/pmc_traffic.json`); kernel stats `prof_*/run_kernel_stats.csv`.', '',
          '| line | workload | value (samples/s) | ms / call | dominant kernel | us / launch step | '
