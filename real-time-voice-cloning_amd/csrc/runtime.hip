@@ -690,8 +690,8 @@ int pack_persist(wrnn_handle* h, int oG2, int oF1, int oF2) {
 //      same list (hops B / C / D split its rows, not its weights)
 //   C  (8 bits): fc3 class cpw w + og, og < cpw
 // with q the dense kernel's block index (columns 4 (16 q + kc) .. + 3). The image exists when
-// every slot's lists fit kPSpZero float4 (90 %-pruned fatchord: ~20 %); otherwise the dense
-// kernels run the zeros (same results, no sparse speed).
+// every slot's lists fit kPSpZero float4 (90 %-pruned fatchord: 6,272, the lists padded to each
+// row group's fullest lane); otherwise the dense kernels run the zeros (same results).
 int pack_persist_sparse(wrnn_handle* h) {
     auto& T = h->host;
     auto& P = h->pw;
@@ -707,6 +707,20 @@ int pack_persist_sparse(wrnn_handle* h) {
     const auto& Wf2 = T["fc2.weight"];
     const auto& Wf3 = T["fc3.weight"];
     auto zero4 = [](const float* p) { return p[0] == 0.f && p[1] == 0.f && p[2] == 0.f && p[3] == 0.f; };
+    {  // live fraction of the step matrices' 1 x 4 blocks (reported with or without an image)
+        long long lv = 0, tot = 0;
+        auto scan = [&](const std::vector<float>& W, int rows, int ld) {
+            for (int r = 0; r < rows; ++r)
+                for (int c = 0; c < kPH; c += 4, ++tot) lv += !zero4(&W[(size_t)r * ld + c]);
+        };
+        scan(Wih2, 3 * H, H + A);
+        scan(Whh1, 3 * H, H);
+        scan(Whh2, 3 * H, H);
+        scan(Wf1, F, H + A);
+        scan(Wf2, F, F + A);
+        scan(Wf3, n, F);
+        P.sp_density = tot ? (double)lv / (double)tot : 1.0;
+    }
     // the block (row pointer, column block q of lane kc) of each set
     auto blkA = [&](int w, int og, int kc, int j, int q) -> const float* {
         const int u = 16 * w + (og & 15), row = j * H + u, k0 = 4 * (16 * q + kc);
@@ -780,7 +794,7 @@ int pack_persist_sparse(wrnn_handle* h) {
     // live MACs per row-step of the pruned step matrices the kernel multiplies (x parts; the aux
     // parts and I are in the per-frame / conditioning GEMMs)
     live_macs = 4.0 * (double)live;
-    P.sp_density = total ? (double)live / (double)total : 1.0;
+    (void)total;
     P.sp_live_macs = live_macs;
     P.sp_live_bytes = (double)live * 18.0;
     int rc = WRNN_OK;
