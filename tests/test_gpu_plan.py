@@ -116,3 +116,43 @@ def test_pruned_c2_plans_by_measured_rates(monkeypatch):
     monkeypatch.setenv('WRNN_SPARSE', '1')
     m.generate_batch_device(mel, True, 11000, 550)
     assert m.sparse_info()['last_call'] and m.plan_info() == [(0, 3, False)] * 3
+
+
+def test_rate_table_beside_the_library_is_loaded_and_overridable(tmp_path, monkeypatch):
+    """The handle plans with rates_mi355x.txt beside the library (the per-build table the
+    measurement pass emits); WRNN_RATES names another file, set_rates overrides
+    keys per handle -- and the plan follows: C2 with 3 rows per group made expensive runs one
+    launch of 4 rows per group."""
+    import os
+    from wavernn_amd import _abi
+    beside = os.path.join(os.path.dirname(_abi.LIB_PATH), 'rates_mi355x.txt')
+    assert os.path.exists(beside)
+    import torch
+    from wavernn_amd.base import hparams_for
+    from wavernn_amd.hparams import sp
+    from wavernn_amd.model import WaveRNN
+    from wavernn_amd.synth import synth_mel, synth_state_dict
+    mt = 'fatchord-wavernn'
+    hp = hparams_for(mt).copy(bits=9)
+
+    def model():
+        m = WaveRNN(hp.rnn_dims, hp.fc_dims, hp.bits, hp.pad, hp.upsample_factors, sp.num_mels,
+                    hp.compute_dims, hp.res_out_dims, hp.res_blocks, sp.hop_size, sp.sample_rate,
+                    mode=hp.mode, model_type=mt, device=0)
+        m.load_state_dict(synth_state_dict(hp, mt, seed=0))
+        return m
+    mel = [torch.from_numpy((synth_mel(1000, 0) / sp.max_abs_value).astype(np.float32)).cuda()]
+    m = model()
+    assert m.rates().splitlines()[0] == '# source: ' + beside
+    m.generate_batch_device(mel, True, 11000, 550)
+    assert m.plan_info() == [(0, 3, False)] * 3
+    m.set_rates('fat9 4.8 5.15 50 6.92')
+    m.generate_batch_device(mel, True, 11000, 550)
+    assert m.plan_info() == [(0, 4, False)]
+    f = tmp_path / 'rates.txt'
+    f.write_text('fat9 4.8 5.15 50 6.92\n')
+    monkeypatch.setenv('WRNN_RATES', str(f))
+    m2 = model()
+    assert m2.rates().splitlines()[0] == '# source: ' + str(f)
+    m2.generate_batch_device(mel, True, 11000, 550)
+    assert m2.plan_info() == [(0, 4, False)]
