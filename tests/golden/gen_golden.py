@@ -95,6 +95,11 @@ CASES = {
                                            43, 8, 1.0, 15, [0, 1, 4000, 7999]),
     'fatchord_mol_pruned_tiny': ('fatchord-wavernn', 'MOL', 9, 24, True, 1000, 100, 44, 9, 1.0, 16,
                                  [0, 1, 700]),
+    # a pruned checkpoint with the trained-like statistics of fatchord_raw9_c2_peaked at C2's full
+    # size. (No geneing case: the reference's own Pruner cannot prune geneing -- its I has
+    # 1 + 80 + 64 = 145 input columns, and mask_from_matrix's reshape into 1 x 4 groups raises.)
+    'fatchord_raw9_c2_pruned_peaked': ('fatchord-wavernn', 'RAW', 9, 1000, True, 11000, 550, 46, 5,
+                                       16.0, 18, [0, 1, 3000, 9000, 12099]),
 }
 # extra weight statistics and parity regime of the trained-like cases (default: 1.0, 1.0,
 # 'bit-exact'); 'store_wav' False keeps a SHA-256 of the f64 waveform instead of the samples
@@ -107,6 +112,7 @@ EXTRA = {
     'fatchord_raw10_pruned_defaults': dict(prune=0.9),
     'runtimeracer_raw10_pruned_defaults': dict(prune=0.9),
     'fatchord_mol_pruned_tiny': dict(prune=0.9),
+    'fatchord_raw9_c2_pruned_peaked': dict(prune=0.9, gru_scale=3.0, fc_scale=2.0, store_wav=False),
 }
 
 
@@ -415,6 +421,9 @@ def main():
             sd_e = synth_state_dict(hp, model_type, seed=wseed, logit_scale=lscale,
                                     gru_scale=ex.get('gru_scale', 1.0),
                                     fc_scale=ex.get('fc_scale', 1.0))
+            if ex.get('prune'):
+                from wavernn_amd.prune import prune_state_dict
+                sd_e = prune_state_dict(sd_e, model_type, z=ex['prune'], group=4)
             out['perturbed_first_div'] = perturbed_first_div(sd_e, hp, model_type, mel, batched,
                                                              tgt, ovl, nseed, res['labels'])
             print(f"{name}: float64-Linear oracle first divergence per fold "

@@ -61,6 +61,13 @@ def test_pruned_fixture_matches_reference_on_the_sparse_path(name, monkeypatch):
         return
     lab = m.last_labels
     assert lab.shape == gold['labels'].shape
+    if meta.get('gru_scale', 1.0) != 1.0:
+        # trained-like statistics: the near-tie gate with its measured allowance
+        # (tests/test_gpu_trained.py, kind 'sparse')
+        from test_gpu_trained import near_tie_gate
+        near_tie_gate(name, 'sparse', meta, gold, lab, wav,
+                      lambda steps: _run(name, monkeypatch, debug_steps=steps)[2])
+        return
     d = np.argwhere(lab != gold['labels'])
     assert len(d) == 0, f'{name}: first divergence (row, step) {d[np.argmin(d[:, 1])] if len(d) else None}'
     assert wave_equal(wav, gold)
