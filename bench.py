@@ -11,6 +11,9 @@ N>1    : one process per GPU (torchrun); utterances are independent, so each ran
          shard (weak scaling, no collective on the data path); the fold rows are gathered to
          rank 0 (one RCCL gather) which post-processes every utterance (wavernn_amd.distributed).
          --utts-per-gpu 8 --gpus 8 is configs[3] (64 utterances on 8 GPUs).
+         --split folds: strong scaling instead -- the --utts-per-gpu utterances of ONE job have
+         their fold rows cut evenly over the N GPUs (single-utterance split, SURVEY §8e;
+         wrnn_set_fold_ranges), the rows gathered to rank 0 as above; a latency mode.
 Also reported: roofline of the dominant recurrent kernel (HIP events on its stream over the
 timed region; HBM, fp32 and latency-floor fractions), the CPU baseline (oracle restatement of
 the reference generate() on this host: the whole utterance on the default thread count, plus
@@ -55,6 +58,10 @@ def parse():
     ap.add_argument('--sparse', default='auto', choices=['auto', '0', '1'],
                     help='block-sparse k_persist instances for pruned weights: by the planner '
                          '(auto), never (0), always (1) -- env WRNN_SPARSE')
+    ap.add_argument('--split', default='utterance', choices=['utterance', 'folds'],
+                    help="N>1 sharding: whole utterances per rank (weak scaling, default) or the "
+                         "fold rows of the job's --utts-per-gpu utterances cut over the ranks "
+                         "(strong scaling: one utterance's latency on N GPUs)")
     ap.add_argument('--engine', default='auto', choices=['auto', 'chain', 'persist'],
                     help='recurrence engine (include/wavernn_mi355x.h WRNN_ENGINE_*)')
     return ap.parse_args()
@@ -277,7 +284,7 @@ def main():
     import torch.distributed as dist
     from wavernn_amd.model import WaveRNN
     from wavernn_amd.base import hparams_for
-    from wavernn_amd.distributed import infer_waveforms, shard
+    from wavernn_amd.distributed import infer_waveforms, shard, shard_folds
     from wavernn_amd.hparams import sp
     from wavernn_amd.synth import synth_state_dict, synth_mel
 
@@ -310,10 +317,15 @@ def main():
     model.set_seed(seed)
     model.set_engine(args.engine)
     U = args.utts_per_gpu
-    n_utts = U * world
+    folds = args.split == 'folds'
+    n_utts = U if folds else U * world  # (fold split: the job's utterances, cut over the ranks)
     # every rank knows every utterance's length; only its own shard is resident in its HBM
     mels_host = [synth_mel(args.frames, seed=i) for i in range(n_utts)]
-    plan = shard([args.frames] * n_utts, world, args.target, args.overlap)
+    if folds:
+        fplan = shard_folds([args.frames] * n_utts, world, args.target, args.overlap)
+        plan = [sorted({u for u, _, _ in p}) for p in fplan]
+    else:
+        plan = shard([args.frames] * n_utts, world, args.target, args.overlap)
     mine = set(plan[rank])
     mels = [torch.from_numpy((m / sp.max_abs_value).astype(np.float32)).to(dev) if i in mine
             else m for i, m in enumerate(mels_host)]
@@ -323,11 +335,12 @@ def main():
     last = {}
     rows_dtype = torch.int16 if model.categorical else torch.float32
 
-    def rows_fn(ms, streams):
+    def rows_fn(ms, streams, ranges=None):
         # streams: the global utterance index offset by the step's base (distributed.py), so
-        # every utterance draws the same noise whatever the world size
+        # every utterance draws the same noise whatever the world size; ranges: this rank's
+        # fold rows of each (split='folds')
         out, roff, _ = model.generate_batch_device(ms, True, args.target, args.overlap,
-                                                   streams=streams)
+                                                   streams=streams, fold_ranges=ranges)
         return out, roff
 
     def post_fn(rows, n_frames):
@@ -339,7 +352,7 @@ def main():
         base = model.get_stream()
         rows = {}
         w = infer_waveforms(mels, rows_fn, post_fn, args.target, args.overlap, S, device=dev,
-                            stream_base=base, dtype=rows_dtype, out_rows=rows)
+                            stream_base=base, dtype=rows_dtype, out_rows=rows, split=args.split)
         model.set_stream(base + n_utts)  # every rank, whatever its shard
         last['base'], last['rows'] = base, rows
         return w
@@ -375,6 +388,9 @@ def main():
     us_rank = None
     info = model.stage_info() if not args.no_timing else []
     rows_per_gpu = U * model.fold_shape(args.frames, True, args.target, args.overlap)[0]
+    if folds:
+        rows_per_gpu = max(sum(hi - lo for _, lo, hi in p) for p in fplan)
+        workload = workload.replace(' per GPU,', f' per job, fold rows split over {world} GPU(s),')
     if info:
         # dominant kernel = largest avg duration x launches
         dom_i = max(range(len(info)), key=lambda i: (info[i][3] if info[i][3] == info[i][3] else 0) * info[i][4])
@@ -471,16 +487,17 @@ def main():
         'metric': 'WaveRNN audio samples/sec (xRTF @16kHz) at 1/2/4/8 MI355X vs CPU ref',
         'value': value, 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'higher_is_better': True, 'scaling': 'strong' if folds and world > 1 else 'weak',
+        'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic (seeded random-init weights of the reference architecture, '
                 'uniform[-4,4] mels)',
         'xrtf': value / sp.sample_rate,
         'config': {'workload': workload,
-                   'utts_per_gpu': U, 'frames': args.frames,
+                   'utts_per_gpu': U, 'frames': args.frames, 'split': args.split,
                    'fold_rows_per_gpu': rows_per_gpu,
-                   'parallelism': (f'utterances sharded over {world} GPU(s); fold rows gathered '
-                                   f'to rank 0 (RCCL gather), f64 post-processing on rank 0'
-                                   if world > 1 else 'one GPU'),
+                   'parallelism': (f'{"fold rows" if folds else "utterances"} sharded over {world} '
+                                   f'GPU(s); fold rows gathered to rank 0 (RCCL gather), f64 '
+                                   f'post-processing on rank 0' if world > 1 else 'one GPU'),
                    'engine': model.last_engine(), 'persist_fallbacks': fb[0],
                    'sparse': {'prune': args.prune, 'image': spi['available'], 'ran': spi['last_call'],
                               'live_block_fraction': spi['density'], 'lds_list_fill_f4': spi['fill_f4']},
@@ -521,7 +538,7 @@ def main():
         # utterance of the LAST rank's shard (gathered over RCCL): the whole-utterance oracle leg
         # is also that utterance's parity check on its global stream (world-size invariance:
         # the same labels as at N = 1)
-        u = plan[world - 1][0]
+        u = plan[world - 1][-1] if folds else plan[world - 1][0]
         stream = last['base'] + u
         result['cpu_baseline'], result['parity'] = cpu_baseline(
             args, sd, hp, mels_host[u], last['rows'][u], wavs[u], seed, stream)

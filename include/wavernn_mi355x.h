@@ -140,6 +140,16 @@ int wrnn_get_stream(wrnn_handle* h, uint32_t* stream);
  * (vocoder/libwavernn/inference.py:106-108, :200-204). A count that does not match the
  * call's n_utts makes that call fail with WRNN_ERR_INVALID. */
 int wrnn_set_utt_streams(wrnn_handle* h, const uint32_t* streams, int n);
+/* Fold range of each utterance of the NEXT wrnn_generate_batch_device call only (n = its
+ * n_utts; n = 0 clears): utterance u runs only its fold rows lo[u] .. hi[u] - 1 (0 <= lo < hi
+ * <= num_folds, batched calls), as rows row_offset[u] .. row_offset[u + 1] - 1 of the output.
+ * Each row computes exactly what it computes in a full call -- same conditioning positions
+ * (fold_with_overlap, fatchord_version.py:290-340), same noise words (Philox keyed by the
+ * global fold index) -- so the fold rows of one utterance can be split over ranks and the
+ * union equals the single-call rows bit for bit (the "one exchange step" single-utterance
+ * split of SURVEY §8e). The reference has no such call: its folds always run as one batch
+ * (fatchord_version.py:180-187). wrnn_generate refuses an armed range. */
+int wrnn_set_fold_ranges(wrnn_handle* h, const int* lo, const int* hi, int n);
 
 /* Fold arithmetic of fold_with_overlap for a mel of n_frames frames
  * (upsampled length L = n_frames * hop). batched=0 -> one row of L steps. */

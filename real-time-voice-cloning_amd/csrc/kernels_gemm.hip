@@ -41,7 +41,7 @@ __device__ __forceinline__ ARow a_row(const GemmA& a, int m, int M) {
         // fold-major rows (m = fold * S + step, M = S * Bu): the 64 rows of a tile are
         // consecutive positions of one or two folds, so each k reads whole cache lines
         const int S = M / a.Bu, f = m / S, t = m - f * S;
-        const int p = f * a.tpo + t;  // fold_with_overlap position
+        const int p = (a.f0 + f) * a.tpo + t;  // fold_with_overlap position
         r.zero |= p >= a.L;                            // zero tail pad
         r.p0 = a.mel;
         r.o0 = p;
@@ -267,7 +267,7 @@ hipError_t launch_mel_stencil(const float* in, int in_pad, int T_in, int W_in, f
 // are uniform over the workgroup (scalar loads). Output: one coalesced 1-KiB store per wave.
 constexpr int kP1Run = 64;
 __global__ __launch_bounds__(kThreads) void k_p1_expand(float4* __restrict__ P1, int Btot,
-                                                        int row0, int S, int tpo, int L, int hop,
+                                                        int row0, int f0, int S, int tpo, int L, int hop,
                                                         int T, int nq, const float4* __restrict__ q,
                                                         const float4* __restrict__ a,
                                                         const float* __restrict__ taps) {
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void k_p1_expand(float4* __restrict__ P1,
     float4 r[5], av = z4;
     int fc = -2;  // frame of the operands in registers (-1: the zero tail pad)
     for (int t = t0; t < t1; ++t) {
-        const int p = fo * tpo + t;  // fold_with_overlap position
+        const int p = (f0 + fo) * tpo + t;  // fold_with_overlap position
         const int f = p < L ? p / hop : -1;
         if (f != fc) {
             fc = f;
@@ -314,14 +314,14 @@ __global__ __launch_bounds__(kThreads) void k_p1_expand(float4* __restrict__ P1,
     }
 }
 
-hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int S, int tpo, int L, int hop,
-                            int T, int nq, const float* q, const float* a, const float* taps,
+hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int f0, int S, int tpo, int L,
+                            int hop, int T, int nq, const float* q, const float* a, const float* taps,
                             hipStream_t s) {
     if (Bu <= 0 || S <= 0 || nq <= 0) return hipSuccess;
     if (hop <= 0 || T <= 0 || Bu > 65535) return hipErrorInvalidValue;
     dim3 grid((nq + kThreads - 1) / kThreads, Bu, (S + kP1Run - 1) / kP1Run);
     hipLaunchKernelGGL(k_p1_expand, grid, dim3(kThreads), 0, s, reinterpret_cast<float4*>(P1), Btot,
-                       row0, S, tpo, L, hop, T, nq, reinterpret_cast<const float4*>(q),
+                       row0, f0, S, tpo, L, hop, T, nq, reinterpret_cast<const float4*>(q),
                        reinterpret_cast<const float4*>(a), taps);
     return hipGetLastError();
 }

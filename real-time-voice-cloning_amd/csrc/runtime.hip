@@ -166,6 +166,7 @@ struct wrnn_handle {
     uint64_t seed = 0;
     uint32_t stream_ctr = 0;
     std::vector<uint32_t> utt_streams;  // wrnn_set_utt_streams: explicit streams of the next call
+    std::vector<int> fold_lo, fold_hi;  // wrnn_set_fold_ranges: fold rows of the next batch call
     // teacher-forced logit gate (wrnn_set_debug_steps): the steps to record, the device map
     // [S] step -> slot and the capture [kDbgSteps][Bp][n] of the last call; dbg_gen keys the
     // captured CHAIN graphs (their k_sample arguments hold the buffers)
@@ -1492,7 +1493,7 @@ int run_resnet(wrnn_handle* h, int n_utts, const float* const* mels, const int* 
 
 // ---- upsample + conditioning for one utterance (its MelResNet output: Rb columns col0..) --
 int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int S, int Btot,
-                 int row0, int fbase, float* P1out, int col0) {
+                 int row0, int fbase, float* P1out, int col0, int f0) {
     auto& ws = h->ws;
     hipStream_t st = h->stream;
     const int H = h->H;
@@ -1541,6 +1542,7 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
         a4.n_aux = h->A - 1;
         a4.Bu = Bu;
         a4.tpo = tpo;
+        a4.f0 = f0;
         b4.kind = 0;
         b4.p = h->WIT;
         b4.ld = H;
@@ -1580,7 +1582,7 @@ int run_upsample(wrnn_handle* h, const float* d_mel, int T, int Bu, int tpo, int
             HIPC(launch_gemm(T + 1, np, h->A - 1, aq, bq, eq, st));
             // the whole stream for the kernels that read it; step 0 only when every launch
             // forms P1 in-kernel (k_persist_init reads step 0)
-            HIPC(launch_p1_expand(P1out, Btot, row0, Bu, h->p1_stream ? S : 1, tpo, L, h->hop, T,
+            HIPC(launch_p1_expand(P1out, Btot, row0, Bu, f0, h->p1_stream ? S : 1, tpo, L, h->hop, T,
                                   np / 4, ws.q4.f() + (size_t)fbase * np,
                                   ws.a4.f() + (size_t)fbase * np, h->pw.p1taps, st));
         } else if (P1out) {  // PERSIST: P1 (step, row) = M1 c + bP1, same gather, same folded layout
@@ -1793,6 +1795,7 @@ void fold_shape(int L, int batched, int target, int overlap, int* B, int* S) {
 
 struct UttPlan {
     int T, L, B, Lpad, pbase, fbase, row0;
+    int f0;  // first fold row of the call (wrnn_set_fold_ranges; 0 otherwise)
 };
 
 // CHAIN engine: per step one launch per stage + the sampler, captured 100 steps per graph.
@@ -3038,11 +3041,19 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     // an unrelated next one
     std::vector<uint32_t> ustreams;
     ustreams.swap(h->utt_streams);
+    std::vector<int> flo, fhi;  // (wrnn_set_fold_ranges: likewise one call's)
+    flo.swap(h->fold_lo);
+    fhi.swap(h->fold_hi);
     if (!h->finalized)
         return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
     if (n_utts <= 0) return fail(WRNN_ERR_INVALID, "n_utts must be positive");
     if (batched && (target <= 0 || overlap < 0))
         return fail(WRNN_ERR_INVALID, "target must be > 0 and overlap >= 0");
+    if (!flo.empty() && ((int)flo.size() != n_utts || !batched))
+        return fail(WRNN_ERR_INVALID, !batched ? "fold ranges need a batched call"
+                                               : "wrnn_set_fold_ranges gave " + std::to_string(flo.size()) +
+                                                     " ranges for a call of " + std::to_string(n_utts) +
+                                                     " utterances");
     std::vector<UttPlan> plan(n_utts);
     int B = 0, S = 0, P = 0, Fr = 0, Tmax = 0;
     for (int u = 0; u < n_utts; ++u) {
@@ -3058,14 +3069,23 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
                                                   : "unbatched utterances of one call must have equal lengths");
         S = s;
         p.B = b;
+        p.f0 = 0;
         p.Lpad = batched ? b * (target + overlap) + overlap : p.L;
+        if (!flo.empty()) {  // a sub-range of the folds; positions stay those of the whole mel
+            if (flo[u] < 0 || fhi[u] <= flo[u] || fhi[u] > b)
+                return fail(WRNN_ERR_INVALID, "fold range [" + std::to_string(flo[u]) + ", " +
+                                                  std::to_string(fhi[u]) + ") of utterance " + std::to_string(u) +
+                                                  " outside its " + std::to_string(b) + " folds");
+            p.f0 = flo[u];
+            p.B = fhi[u] - flo[u];
+        }
         p.pbase = P;
         // frame slots: [guard][zero frame = fbase][T frames][guard][guard], consecutive
         // utterances sharing one guard: the in-kernel P1 taps (frames f-2 .. f+2) then read
         // zero rows past either end without bounds checks
         p.fbase = Fr + 1;
         p.row0 = B;
-        B += b;
+        B += p.B;
         P += p.Lpad;
         Fr += p.T + 3;
         Tmax = std::max(Tmax, p.T);
@@ -3141,11 +3161,11 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
         const UttPlan& p = plan[u];
         for (int f = 0; f < p.B; ++f) {
             RowInfo& ri = rows[p.row0 + f];
-            ri.rel0 = batched ? f * (target + overlap) : 0;
+            ri.rel0 = batched ? (p.f0 + f) * (target + overlap) : 0;
             ri.pos0 = p.pbase + ri.rel0;
             ri.L = p.L;
             ri.fbase = p.fbase;
-            ri.fold = f;
+            ri.fold = p.f0 + f;  // the global fold index keys the noise
             ri.stream = ustreams.empty() ? h->stream_ctr + (uint32_t)u : ustreams[u];
         }
         if (row_offset) row_offset[u] = p.row0;
@@ -3181,7 +3201,8 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
     CHECK(run_resnet(h, n_utts, mels, Ts.data(), col0.data(), Tsum));
     for (int u = 0; u < n_utts; ++u)
         CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0, S, Bp,
-                           plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr, col0[u]));
+                           plan[u].row0, plan[u].fbase, use_p ? h->pws.P1.f() : nullptr, col0[u],
+                           plan[u].f0));
     int rc = WRNN_OK;
     if (use_p) {
         rc = run_persist(h, S, cb, user);
@@ -3204,7 +3225,7 @@ int generate_impl(wrnn_handle* h, int n_utts, const float* const* mels, const in
             if (h->pw.p1x4)  // cI was not written (P1 carried it): conditioning again, cI only
                 for (int u = 0; u < n_utts; ++u)
                     CHECK(run_upsample(h, mels[u], plan[u].T, plan[u].B, batched ? target + overlap : 0,
-                                       S, Bp, plan[u].row0, plan[u].fbase, nullptr, col0[u]));
+                                       S, Bp, plan[u].row0, plan[u].fbase, nullptr, col0[u], plan[u].f0));
             h->last_B = Bp;  // chain runs every padded row (cI stride is Bp)
             rc = run_chain(h, S, cb, user);
             h->last_B = B;
@@ -3420,6 +3441,14 @@ int wrnn_set_utt_streams(wrnn_handle* h, const uint32_t* streams, int n) {
     return WRNN_OK;
 }
 
+int wrnn_set_fold_ranges(wrnn_handle* h, const int* lo, const int* hi, int n) {
+    if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    if (n < 0 || (n > 0 && (!lo || !hi))) return fail(WRNN_ERR_INVALID, "bad fold range list");
+    h->fold_lo.assign(lo, lo + n);
+    h->fold_hi.assign(hi, hi + n);
+    return WRNN_OK;
+}
+
 int wrnn_fold_shape(int n_frames, int hop_length, int batched, int target, int overlap,
                     int* num_folds, int* seq_len) {
     if (!num_folds || !seq_len) return fail(WRNN_ERR_INVALID, "null argument");
@@ -3429,14 +3458,32 @@ int wrnn_fold_shape(int n_frames, int hop_length, int batched, int target, int o
     return WRNN_OK;
 }
 
+// The one-call options (wrnn_set_utt_streams, wrnn_set_fold_ranges) belong to the next
+// generate call whatever its outcome, also when it fails before generate_impl takes them.
+struct DisarmOnExit {
+    wrnn_handle* h;
+    ~DisarmOnExit() {
+        if (!h) return;
+        h->utt_streams.clear();
+        h->fold_lo.clear();
+        h->fold_hi.clear();
+    }
+};
+
 int wrnn_generate(wrnn_handle* h, const float* mel, int n_frames, int batched, int target,
                   int overlap, int16_t* labels, float* samples, size_t capacity, int* num_folds,
                   int* seq_len, wrnn_progress_fn cb, void* user) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    DisarmOnExit disarm{h};
     if (!h->finalized)
         return fail(WRNN_ERR_NOT_LOADED, "Model hasn't been loaded. Call loadWeights first.");
     if (!mel || n_frames <= 0) return fail(WRNN_ERR_INVALID, "empty mel");
     if (labels && h->cfg.mode != WRNN_MODE_RAW) return fail(WRNN_ERR_INVALID, "labels require RAW mode");
+    if (!h->fold_lo.empty()) {
+        h->fold_lo.clear();
+        h->fold_hi.clear();
+        return fail(WRNN_ERR_INVALID, "fold ranges apply to wrnn_generate_batch_device only");
+    }
     HIPC(hipSetDevice(h->device));
     int B, S;
     fold_shape(n_frames * h->hop, batched, target, overlap, &B, &S);
@@ -3474,15 +3521,18 @@ int wrnn_generate_batch_device(wrnn_handle* h, int n_utts, const float* const* m
                                int16_t* labels_dev, float* samples_dev, size_t capacity,
                                int* row_offset, int* seq_len, wrnn_progress_fn cb, void* user) {
     if (!h) return fail(WRNN_ERR_INVALID, "null handle");
+    DisarmOnExit disarm{h};
     if (!mels || !n_frames || !row_offset) return fail(WRNN_ERR_INVALID, "null argument");
     if (labels_dev && h->cfg.mode != WRNN_MODE_RAW)
         return fail(WRNN_ERR_INVALID, "labels require RAW mode");
     HIPC(hipSetDevice(h->device));
     int B = 0, S = 0;
+    const bool ranged = !h->fold_lo.empty() && (int)h->fold_lo.size() == n_utts;
     for (int u = 0; u < n_utts; ++u) {
         int b, s;
         if (n_frames[u] <= 0) return fail(WRNN_ERR_INVALID, "empty mel");
         fold_shape(n_frames[u] * h->hop, batched, target, overlap, &b, &s);
+        if (ranged) b = std::max(0, std::min(h->fold_hi[u], b) - std::max(h->fold_lo[u], 0));
         B += b;
         S = s;
     }

@@ -118,6 +118,7 @@ struct GemmA {  // A(m, k)
     const float* R;
     int ldr, r_off, n_aux;
     int Bu, tpo;
+    int f0;  // kind 1: fold index of row block 0 (wrnn_set_fold_ranges): p = (f0 + f) * tpo + t
 };
 struct GemmB {  // B(k, n)
     int kind;   // 0: row-major [k*ld + n]; 1: im2col of the zero-padded mel (conv_in)
@@ -154,8 +155,9 @@ hipError_t launch_fill_rows(float* dst, const float* src, int n, int rows, hipSt
 // P1 [t][Btot][4 nq] of fold rows row0 .. row0 + Bu - 1 from the per-frame projections q / a
 // ([1 + T][4 nq], slot 0 = zero frame) and the upsampler's per-phase taps [hop][8] (runtime.hip
 // pack_p1): P1(p = hop f + s) = sum_k taps[s][k] q(f - 2 + k) + a(f), a(zero frame) for p >= L.
-hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int S, int tpo, int L, int hop,
-                            int T, int nq, const float* q, const float* a, const float* taps,
+// Fold rows are f0 .. f0 + Bu - 1 of the utterance (positions (f0 + fo) * tpo + t).
+hipError_t launch_p1_expand(float* P1, int Btot, int row0, int Bu, int f0, int S, int tpo, int L,
+                            int hop, int T, int nq, const float* q, const float* a, const float* taps,
                             hipStream_t s);
 
 // ---------------------------------------------------------------------------------------

@@ -39,7 +39,7 @@ EXPORTED = [
     'wrnn_set_engine', 'wrnn_last_engine', 'wrnn_bin_read', 'wrnn_load_bin',
     'wrnn_de_emphasis', 'wrnn_post_overlaps', 'wrnn_post_assemble', 'wrnn_fallback_info',
     'wrnn_debug_beta', 'wrnn_debug_decide', 'wrnn_debug_rot_plan', 'wrnn_debug_slice_plan', 'wrnn_rot_info', 'wrnn_persist_steps', 'wrnn_plan_info', 'wrnn_debug_p1', 'wrnn_get_stream',
-    'wrnn_set_utt_streams', 'wrnn_set_debug_steps', 'wrnn_debug_logits', 'wrnn_debug_wide_layout',
+    'wrnn_set_utt_streams', 'wrnn_set_fold_ranges', 'wrnn_set_debug_steps', 'wrnn_debug_logits', 'wrnn_debug_wide_layout',
     'wrnn_sparse_info', 'wrnn_set_rates', 'wrnn_get_rates', 'wrnn_debug_plan',
 ]
 
@@ -108,6 +108,7 @@ def load_library(path=None):
         'wrnn_set_stream': (c_int, [c_void_p, ctypes.c_uint32]),
         'wrnn_get_stream': (c_int, [c_void_p, P(ctypes.c_uint32)]),
         'wrnn_set_utt_streams': (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
+        'wrnn_set_fold_ranges': (c_int, [c_void_p, P(c_int), P(c_int), c_int]),
         'wrnn_fold_shape': (c_int, [c_int, c_int, c_int, c_int, c_int, P(c_int), P(c_int)]),
         'wrnn_generate': (c_int, [c_void_p, P(ctypes.c_float), c_int, c_int, c_int, c_int,
                                   P(ctypes.c_int16), P(ctypes.c_float), c_size_t, P(c_int),

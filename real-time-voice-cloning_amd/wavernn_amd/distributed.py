@@ -13,6 +13,15 @@ waveforms; the other ranks get None.
 ``shard(lengths, world)`` balances by work: every utterance costs S = target + 2*overlap
 sequential steps regardless of length, and its number of fold rows grows with length, so the
 greedy longest-first assignment balances rows per rank.
+
+``split='folds'`` shards fold ROWS instead (``shard_folds``): the utterance-major list of all
+fold rows is cut into ``world`` contiguous, equal pieces, so one utterance can span ranks -- the
+single-utterance split of SURVEY §8e (fold groups per GPU, then the one gather). A rank runs
+its pieces with ``wrnn_set_fold_ranges``; every row computes what it computes in a whole-
+utterance call (conditioning positions and noise are keyed by the global fold index), so the
+gathered rows, and the waveforms, equal the single-GPU ones bit for bit. Its use is latency:
+a 1000-frame utterance's 18 rows on 2 GPUs run at 9 rows per GPU, on 3 or more at <= 6, where
+every XCD group carries one row.
 """
 from concurrent.futures import ThreadPoolExecutor
 
@@ -42,8 +51,26 @@ def shard(n_frames, world, target, overlap, hop=200):
     return out
 
 
+def shard_folds(n_frames, world, target, overlap, hop=200):
+    """Fold-row sharding: rank r gets global rows [r R / world, (r + 1) R / world) of the
+    utterance-major row list (R = all fold rows); returns per rank a list of (utt, lo, hi)
+    segments, fold rows lo .. hi - 1 of utterance utt, in row order."""
+    nf = [fold_rows(T, target, overlap, hop) for T in n_frames]
+    R = sum(nf)
+    cuts = [r * R // world for r in range(world + 1)]
+    out = [[] for _ in range(world)]
+    base = 0
+    for u, n in enumerate(nf):
+        for r in range(world):
+            lo, hi = max(cuts[r], base), min(cuts[r + 1], base + n)
+            if lo < hi:
+                out[r].append((u, lo - base, hi - base))
+        base += n
+    return out
+
+
 def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, device=None,
-                    dst=0, threads=8, stream_base=0, dtype=None, out_rows=None):
+                    dst=0, threads=8, stream_base=0, dtype=None, out_rows=None, split='utterance'):
     """Vocode a list of mels across the ranks of the default process group.
 
     ``rows_fn(list_of_mels, streams) -> (rows, row_offsets)``: this rank's fold recurrence,
@@ -54,6 +81,9 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
     output does not depend on the world size (the reference's CPU backend seeds every worker
     explicitly, vocoder/libwavernn/inference.py:106-108, :200-204). Callers advance their own
     stream counter by ``len(mels)`` afterwards, on every rank.
+    ``split``: 'utterance' (whole utterances per rank, the default) or 'folds' (``shard_folds``;
+    ``rows_fn`` then takes a third argument, the [(lo, hi)] fold range of each mel it is handed,
+    and returns the rows of those ranges in order).
     ``post_fn(rows_np, n_frames) -> f64 waveform``: the host post-processing of one utterance
     (``WaveRNN.postprocess_rows``). ``dtype``: the rows' torch dtype (int16 for categorical
     models, float32 for MOL / Beta) -- every rank must gather buffers of the same byte size,
@@ -69,7 +99,12 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
     dtype = dtype if dtype is not None else torch.int16
     if not mels:  # every rank sees the same (empty) list: nothing to run or gather
         return [] if rank == dst or world == 1 else None
+    if split not in ('utterance', 'folds'):
+        raise ValueError(f"split must be 'utterance' or 'folds', not {split!r}")
     frames = [int(m.shape[-1]) for m in mels]
+    if split == 'folds':
+        return _infer_fold_split(mels, frames, rows_fn, post_fn, target, overlap, seq_len, hop,
+                                 device, dst, threads, stream_base, dtype, out_rows, world, rank)
     plan = shard(frames, world, target, overlap, hop)
     rows_of = [sum(fold_rows(frames[i], target, overlap, hop) for i in p) for p in plan]
     mine = plan[rank]
@@ -115,6 +150,50 @@ def infer_waveforms(mels, rows_fn, post_fn, target, overlap, seq_len, hop=200, d
     for i, w in zip([j[0] for j in jobs], _map(lambda j: post_fn(j[1], frames[j[0]]), jobs, threads)):
         out[i] = w
     return out
+
+
+def _infer_fold_split(mels, frames, rows_fn, post_fn, target, overlap, seq_len, hop, device, dst,
+                      threads, stream_base, dtype, out_rows, world, rank):
+    import torch
+    import torch.distributed as dist
+    plan = shard_folds(frames, world, target, overlap, hop)
+    nf = [fold_rows(T, target, overlap, hop) for T in frames]
+    mine = plan[rank]
+    if mine:
+        rows, _ = rows_fn([mels[u] for u, _, _ in mine], [stream_base + u for u, _, _ in mine],
+                          [(lo, hi) for _, lo, hi in mine])
+        if rows.dtype != dtype:
+            raise TypeError(f'rows_fn returned {rows.dtype}, expected {dtype}')
+        if rows.shape[0] != sum(hi - lo for _, lo, hi in mine):
+            raise ValueError(f'rows_fn returned {rows.shape[0]} rows for fold ranges {mine}')
+    else:
+        rows = None
+    if world == 1:
+        parts = [rows.cpu().numpy()]
+    else:
+        width = max(sum(hi - lo for _, lo, hi in p) for p in plan)
+        dev = device if device is not None else (rows.device if rows is not None else torch.device('cpu'))
+        if dist.get_backend() == 'gloo':
+            dev = torch.device('cpu')
+        buf = torch.zeros((width, seq_len), dtype=dtype, device=dev)
+        if rows is not None:
+            buf[:rows.shape[0]] = rows
+        wire = buf.view(torch.uint8)
+        bufs = [torch.empty_like(wire) for _ in range(world)] if rank == dst else None
+        dist.gather(wire, bufs, dst=dst)
+        if rank != dst:
+            return None
+        parts = [b.view(dtype).cpu().numpy() for b in bufs]
+    full = [np.empty((n, seq_len), dtype=parts[0].dtype) for n in nf]
+    for r in range(world):
+        at = 0
+        for u, lo, hi in plan[r]:
+            full[u][lo:hi] = parts[r][at:at + hi - lo]
+            at += hi - lo
+    if out_rows is not None:
+        for u in range(len(mels)):
+            out_rows[u] = full[u]
+    return _map(lambda u: post_fn(full[u], frames[u]), range(len(mels)), threads)
 
 
 _POOL = {}

@@ -187,6 +187,16 @@ class WaveRNN:
         arr = (ctypes.c_uint32 * len(streams))(*streams)
         _abi.check(self._lib.wrnn_set_utt_streams(self._h, arr, len(streams)))
 
+    def _set_fold_ranges(self, ranges, n_utts):
+        if ranges is None:
+            return
+        ranges = [(int(lo), int(hi)) for lo, hi in ranges]
+        if len(ranges) != n_utts:
+            raise ValueError(f'{len(ranges)} fold ranges for {n_utts} utterances')
+        lo = (ctypes.c_int * n_utts)(*[r[0] for r in ranges])
+        hi = (ctypes.c_int * n_utts)(*[r[1] for r in ranges])
+        _abi.check(self._lib.wrnn_set_fold_ranges(self._h, lo, hi, n_utts))
+
     def fold_shape(self, n_frames, batched, target, overlap):
         b, s = ctypes.c_int(), ctypes.c_int()
         _abi.check(self._lib.wrnn_fold_shape(int(n_frames), self.hop_length, int(bool(batched)),
@@ -364,18 +374,23 @@ class WaveRNN:
         return labels, samples, B, S
 
     def generate_batch_device(self, mels_dev, batched, target, overlap, progress_callback=None,
-                              streams=None):
+                              streams=None, fold_ranges=None):
         """Several utterances as one batch of fold rows, inputs resident in HBM.
 
         ``mels_dev``: list of torch CUDA float32 tensors (feat_dims, T_u) on this model's device
         (already normalised). Returns (out_dev, row_offset, S): ``out_dev`` is a torch CUDA
         tensor (rows, S) -- int16 labels (RAW) or float32 samples (MOL). ``streams``: explicit
         noise stream per utterance (default: the handle's counter + u; wrnn_set_utt_streams).
+        ``fold_ranges``: [(lo, hi)] per utterance -- run only fold rows lo .. hi - 1 of it
+        (wrnn_set_fold_ranges: the rows equal those of a full call bit for bit).
         """
         import torch
         if not self._loaded:
             raise RuntimeError("Model hasn't been loaded. Call loadWeights first.")
         n = len(mels_dev)
+        for name, lst in (('streams', streams), ('fold ranges', fold_ranges)):
+            if lst is not None and len(lst) != n:  # (before either list is armed on the handle)
+                raise ValueError(f'{len(lst)} {name} for {n} utterances')
         mels_dev = [m.contiguous() for m in mels_dev]
         for m in mels_dev:
             if m.dtype != torch.float32 or not m.is_cuda:
@@ -384,8 +399,11 @@ class WaveRNN:
         ptrs = (ctypes.c_void_p * n)(*[m.data_ptr() for m in mels_dev])
         rows = 0
         S = 0
-        for m in mels_dev:
+        for u, m in enumerate(mels_dev):
             b, S = self.fold_shape(int(m.shape[-1]), batched, target, overlap)
+            if fold_ranges is not None and u < len(fold_ranges):
+                lo, hi = fold_ranges[u]
+                b = max(0, min(int(hi), b) - max(int(lo), 0))
             rows += b
         dev = mels_dev[0].device
         if self.categorical:
@@ -400,6 +418,7 @@ class WaveRNN:
         torch.cuda.current_stream(dev).synchronize()
         fb0 = self.fallback_info()[0]
         self._set_utt_streams(streams, n)
+        self._set_fold_ranges(fold_ranges, n)
         rc = self._lib.wrnn_generate_batch_device(
             self._h, n, ptrs, frames, int(bool(batched)), int(target or 0), int(overlap or 0),
             lab_p, smp_p, rows * S, roff, ctypes.byref(s_out), cfn, None)

@@ -42,7 +42,7 @@ FRAMES = {'RAW': [22, 30, 25], 'MOL': [24, 21]}
 STREAM_BASE = 7  # the callers' stream counter before the call (bench: model.get_stream())
 
 
-def _worker(rank, world, port, q, mode):
+def _worker(rank, world, port, q, mode, split='utterance'):
     import sys
     import torch
     import torch.distributed as dist
@@ -65,12 +65,16 @@ def _worker(rank, world, port, q, mode):
     raw = mode == 'RAW'
     ran = []
 
-    def rows_fn(ms, streams):
-        # one stream per utterance of the GLOBAL list, as WaveRNN.generate_batch_device gets it
-        ran.extend(streams)
+    def rows_fn(ms, streams, ranges=None):
+        # one stream per utterance of the GLOBAL list, as WaveRNN.generate_batch_device gets it;
+        # fold split: the rows lo .. hi - 1 of each (the ABI's wrnn_set_fold_ranges contract,
+        # pinned against whole calls on the GPU by test_gpu_fold_split.py)
+        ran.extend(streams if ranges is None else list(zip(streams, ranges)))
         outs = [oracle_infer_waveform(sd, hp, 'fatchord-wavernn', m, target=400, overlap=50,
                                       seed=5, stream=s, post=False)['labels' if raw else 'samples']
                 for m, s in zip(ms, streams)]
+        if ranges is not None:
+            outs = [o[lo:hi] for o, (lo, hi) in zip(outs, ranges)]
         roff = np.cumsum([0] + [o.shape[0] for o in outs]).tolist()
         return torch.from_numpy(np.concatenate(outs)), roff
 
@@ -82,7 +86,8 @@ def _worker(rank, world, port, q, mode):
         return postprocess(rows, True, 400, 50, False, True, 30, (n_frames - 1) * 200, 200,
                            lib=lib)
     wavs = infer_waveforms(mels, rows_fn, post_fn, 400, 50, seq_len=500,
-                           stream_base=STREAM_BASE, dtype=torch.int16 if raw else torch.float32)
+                           stream_base=STREAM_BASE, dtype=torch.int16 if raw else torch.float32,
+                           split=split)
     q.put((rank, sorted(ran)))
     if rank == 0:
         q.put([w.tolist() for w in wavs])
@@ -91,11 +96,11 @@ def _worker(rank, world, port, q, mode):
     dist.destroy_process_group()
 
 
-def _run(world, mode):
+def _run(world, mode, split='utterance'):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, split)) for r in range(world)]
     for p in procs:
         p.start()
     streams, got = {}, None
@@ -145,3 +150,48 @@ def test_three_ranks_two_mol_utterances_empty_shard():
 def test_empty_utterance_list():
     from wavernn_amd.distributed import infer_waveforms
     assert infer_waveforms([], None, None, 400, 50, seq_len=500) == []
+
+
+def test_shard_folds_cuts_rows_evenly():
+    from wavernn_amd.distributed import shard_folds, fold_rows
+    frames = [1000, 200, 1000, 50, 700]
+    nf = [fold_rows(f, 11000, 550) for f in frames]
+    for world in (1, 2, 3, 4, 8, 64):
+        plan = shard_folds(frames, world, 11000, 550)
+        sizes = [sum(hi - lo for _, lo, hi in p) for p in plan]
+        assert max(sizes) - min(sizes) <= 1 and sum(sizes) == sum(nf)
+        # every fold row of every utterance exactly once, in utterance-major order
+        flat = [(u, f) for p in plan for u, lo, hi in p for f in range(lo, hi)]
+        assert flat == [(u, f) for u, n in enumerate(nf) for f in range(n)]
+    # one 1000-frame utterance (C2: 18 rows) over 2 / 4 ranks
+    assert shard_folds([1000], 2, 11000, 550) == [[(0, 0, 9)], [(0, 9, 18)]]
+    assert [sum(hi - lo for _, lo, hi in p) for p in shard_folds([1000], 4, 11000, 550)] == [4, 5, 4, 5]
+
+
+def test_two_rank_fold_split_equals_single_process():
+    """split='folds': the 3 RAW utterances' fold rows cut evenly over 2 ranks (one utterance
+    spans both), gathered and re-assembled on rank 0 -- waveforms == one process bit for bit,
+    and each rank ran the ranges shard_folds assigned it."""
+    from wavernn_amd.distributed import shard_folds
+    streams, got = _run(2, 'RAW', split='folds')
+    ref = _single_process('RAW')
+    plan = shard_folds(FRAMES['RAW'], 2, 400, 50)
+    for r in range(2):
+        assert streams[r] == sorted((STREAM_BASE + u, (lo, hi)) for u, lo, hi in plan[r])
+    assert any(u == plan[1][0][0] for u, _, _ in plan[0])  # an utterance spans the ranks
+    for i in range(len(FRAMES['RAW'])):
+        assert np.array_equal(np.asarray(got[i]), ref[i])
+
+
+def test_three_rank_fold_split_mol():
+    streams, got = _run(3, 'MOL', split='folds')
+    ref = _single_process('MOL')
+    for i in range(len(FRAMES['MOL'])):
+        assert np.array_equal(np.asarray(got[i]), ref[i])
+
+
+def test_fold_split_rejects_unknown_mode():
+    from wavernn_amd.distributed import infer_waveforms
+    with pytest.raises(ValueError):
+        infer_waveforms([np.zeros((80, 30), np.float32)], None, None, 400, 50, seq_len=500,
+                        split='rows')
