@@ -67,6 +67,7 @@ constexpr int L_XH2 = L_X1 + kPNR * kPH;            // [kPNR][512] h2 (staged at
 constexpr int L_RED = L_XH2 + kPNR * kPH;           // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
+constexpr int L_ARR = L_SX + 13;                    // stage-A arrivals of waves 0-3 (uint, monotonic)
 
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
@@ -347,7 +348,10 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             }
         }
     };
-    if (tid == 0) lds[L_FAIL] = 0.f;
+    if (tid == 0) {
+        lds[L_FAIL] = 0.f;
+        reinterpret_cast<unsigned*>(lds)[L_ARR] = 0u;
+    }
     if constexpr (P1R) {  // ring prologue: P1(t0 + 1), read by GRU1 of step t0
         __syncthreads();  // RowInfo in LDS
         p1_loads(a.t0 + 1);
@@ -434,6 +438,11 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                         v, xr, (unsigned)((((t & 1) * kPNR + lr) * kPH + u) * 4) * 4u, XB_G * 4, 0);
                 }
             }
+            // this wave's reads of X0 (x1) are done (and its publishes issued): hop A may
+            // overwrite X0 once all four GRU2 waves have arrived (x0_free below)
+            if (gate_a && (tid & 63) == 0)
+                __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(lds) + L_ARR, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __builtin_amdgcn_s_setprio(0);
         XSTAMP(30);
@@ -445,6 +454,29 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
         // h2 only and each poll lane forms x2 = x1 + h2 of its couples itself -- the producer's
         // own fp32 add on the same operands (bit-identical x2), one publish instead of two, and
         // no second poll for h2. (Polling x2 with all 8 waves measured slower: 6.38 vs 6.28 us.)
+        // X0 holds x1 until every GRU2 wave (0-3) has finished its stage-A products: a wave whose
+        // hop-A poll completes early (its producer slots were ahead, e.g. at the launch's first
+        // step) must not overwrite couples that a slower wave of this workgroup still reads
+        // (the sparse instances' per-lane work differs between waves). Waves 0-3 only; normally
+        // satisfied on the first read.
+        // (the counter is read once before the poll: when the four waves have arrived by then,
+        // as they normally have, nothing is waited for after it)
+        const unsigned arr_want = 4u * (unsigned)(t - a.t0 + 1);
+        const bool arr_early = wv_lo && __hip_atomic_load(reinterpret_cast<const unsigned*>(lds) + L_ARR,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= arr_want;
+        auto x0_free = [&]() {
+            const unsigned want = arr_want;
+            const unsigned* arr = reinterpret_cast<const unsigned*>(lds) + L_ARR;
+            if (arr_early) return;
+            const unsigned t0s = p_now();
+            while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+                __builtin_amdgcn_s_sleep(1);
+                if (p_now() - t0s > kSpinTicks) {  // (unreachable: every wave 0-3 arrives)
+                    lds[L_FAIL] = 1.f;
+                    break;
+                }
+            }
+        };
         if (X2L) {
             if (wv_lo) {
                 unsigned off[NR];
@@ -455,6 +487,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                     dst[m] = reinterpret_cast<float2*>(lds + L_XH2 + m * kPH) + tl;
                 }
                 if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
+                x0_free();
 #pragma unroll
                 for (int m = 0; m < NR; ++m) {  // x2 = x1 + h2 of the same couples (own writes)
                     float2* x = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
@@ -473,6 +506,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                 off[m] = (unsigned)(m * 5 * kPH + 2 * tl) * 8u;
                 dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
             }
+            x0_free();  // (the poll writes X0 itself)
             if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();

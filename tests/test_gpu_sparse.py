@@ -21,6 +21,9 @@ from conftest import golden_case, golden_meta, is_continuous, wave_equal
 pytestmark = pytest.mark.gpu
 
 PRUNED = sorted(k for k, v in golden_meta().items() if v.get('prune'))
+# the sparse instances are fatchord k_persist ones; a pruned runtimeracer model runs its dense
+# kernels (test_pruned_fixture_matches_reference_on_the_sparse_path)
+PRUNED_FAT = [k for k in PRUNED if golden_meta()[k]['model_type'] == 'fatchord-wavernn']
 
 
 def _run(name, monkeypatch, sparse=True, debug_steps=None, nr_max=None):
@@ -54,6 +57,8 @@ def test_pruned_fixture_matches_reference_on_the_sparse_path(name, monkeypatch):
     if meta['model_type'] == 'fatchord-wavernn':
         assert info['available'] and info['last_call'], info
         assert info['density'] < 0.2, info
+    else:  # no sparse instances for this topology: forced sparse runs its dense kernels
+        assert not info['last_call'], info
     if is_continuous(meta):
         s = m.last_samples
         assert float(np.sqrt(np.mean((s.astype(np.float64) - gold['samples']) ** 2))) <= 1e-4
@@ -73,13 +78,11 @@ def test_pruned_fixture_matches_reference_on_the_sparse_path(name, monkeypatch):
     assert wave_equal(wav, gold)
 
 
-@pytest.mark.parametrize('name', PRUNED)
+@pytest.mark.parametrize('name', PRUNED_FAT)
 def test_sparse_equals_dense_bit_for_bit(name, monkeypatch):
     """Same weights, sparse vs dense k_persist (same plan): identical labels / samples and
     identical teacher-forced logits (the sparse sums skip only exact-zero products)."""
     meta, gold = golden_case(name)
-    if meta['model_type'] != 'fatchord-wavernn':
-        pytest.skip('sparse instances: fatchord k_persist')
     steps = [int(s) for s in gold['logits_steps']][:4]
     _, _, ms, _ = _run(name, monkeypatch, sparse=True, debug_steps=steps)
     _, _, md, _ = _run(name, monkeypatch, sparse=False, debug_steps=steps)
