@@ -183,11 +183,27 @@ def test_two_rank_fold_split_equals_single_process():
         assert np.array_equal(np.asarray(got[i]), ref[i])
 
 
-def test_three_rank_fold_split_mol():
-    streams, got = _run(3, 'MOL', split='folds')
-    ref = _single_process('MOL')
-    for i in range(len(FRAMES['MOL'])):
-        assert np.array_equal(np.asarray(got[i]), ref[i])
+def test_fold_split_single_process_reassembles_float_rows():
+    """split='folds' without a process group (world 1) on float32 (MOL-type) rows: rows_fn sees
+    every utterance's whole range and post_fn gets each utterance's rows back in fold order."""
+    import torch
+    from wavernn_amd.distributed import infer_waveforms, fold_rows
+    frames = [30, 22, 41]
+    nf = [fold_rows(T, 400, 50) for T in frames]
+    mels = [np.zeros((80, T), np.float32) for T in frames]
+    seen = []
+
+    def rows_fn(ms, streams, ranges):
+        seen.append((streams, ranges))
+        # row f of utterance u holds u * 100 + f in every step
+        return torch.cat([torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 500) + 100 * (s - 3)
+                          for s, (lo, hi) in zip(streams, ranges)]), None
+
+    got = infer_waveforms(mels, rows_fn, lambda rows, T: rows[:, 0].copy(), 400, 50, seq_len=500,
+                          stream_base=3, dtype=torch.float32, split='folds')
+    assert seen == [([3, 4, 5], [(0, n) for n in nf])]
+    for u, n in enumerate(nf):
+        assert np.array_equal(got[u], 100 * u + np.arange(n, dtype=np.float32))
 
 
 def test_fold_split_rejects_unknown_mode():
