@@ -441,8 +441,8 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             // this wave's reads of X0 (x1) are done (and its publishes issued): hop A may
             // overwrite X0 once all four GRU2 waves have arrived (x0_free below)
             if (gate_a && (tid & 63) == 0)
-                __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(lds) + L_ARR, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(lds) + L_ARR, 1u, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);  // (orders this wave's X0 reads before it)
         }
         __builtin_amdgcn_s_setprio(0);
         XSTAMP(30);
@@ -463,13 +463,13 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
         // as they normally have, nothing is waited for after it)
         const unsigned arr_want = 4u * (unsigned)(t - a.t0 + 1);
         const bool arr_early = wv_lo && __hip_atomic_load(reinterpret_cast<const unsigned*>(lds) + L_ARR,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= arr_want;
+                                                          __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= arr_want;
         auto x0_free = [&]() {
             const unsigned want = arr_want;
             const unsigned* arr = reinterpret_cast<const unsigned*>(lds) + L_ARR;
             if (arr_early) return;
             const unsigned t0s = p_now();
-            while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+            while (__hip_atomic_load(arr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
                 __builtin_amdgcn_s_sleep(1);
                 if (p_now() - t0s > kSpinTicks) {  // (unreachable: every wave 0-3 arrives)
                     lds[L_FAIL] = 1.f;
