@@ -68,6 +68,12 @@ constexpr int L_RED = L_XH2 + kPNR * kPH;           // [32 og][kPNR][2]
 constexpr int L_SX = L_RED + kPCls * kPNR * 2;      // sampled x per row
 constexpr int L_FAIL = L_SX + 12;                   // set when a tagged poll gave up
 constexpr int L_ARR = L_SX + 13;                    // stage-A arrivals of waves 0-3 (uint, monotonic)
+// x2 of a launch with NR < kPNR rows per group: row r in the unused last row slot of X0 / X1 / XH2
+// (row stride kPNR * kPH floats), so hop A never writes over the x1 that stage A reads
+constexpr int L_X2 = L_X0 + (kPNR - 1) * kPH;
+static_assert(L_X1 == L_X0 + kPNR * kPH && L_XH2 == L_X1 + kPNR * kPH &&
+                  L_X2 + (kPNR - 2) * kPNR * kPH + kPH == L_XH2 + kPNR * kPH,
+              "x2 rows 0 .. kPNR - 2 sit in the last row slots of X0, X1, XH2");
 
 constexpr int L_GH2 = L_SX + 16;                    // gh2 = W_hh2 h2 + b_hh2 [16 units][3][kPNR]
 constexpr int L_RI = L_GH2 + 16 * 3 * kPNR;         // RowInfo of the group's rows (6 words each)
@@ -93,7 +99,7 @@ static_assert(L_TOTAL * 4 + 64 <= 160 * 1024, "LDS carve exceeds the CU's 160 Ki
 // sees its live blocks in increasing q -- the dense kernel's order minus products that are exact
 // zeros -- so the sums are bit-identical to the dense kernel's on the same weights.
 // RM: the rows (bit r) accumulated.
-template <int NR, int G, int RM = 0xF>
+template <int NR, int G, int RM = 0xF, int XSTR = kPK4>
 __device__ __forceinline__ void sp_products(const float4* Wsp, const float4* Xs, unsigned (&m)[G],
                                             unsigned (&p)[G], const int kc, v2f (&acc)[NR][G]) {
     const unsigned zb = (unsigned)(kPSpZero + kc);
@@ -116,7 +122,7 @@ __device__ __forceinline__ void sp_products(const float4* Wsp, const float4* Xs,
         // reported as not applied once the row mask has removed rows)
         for (int r = 0; r < NR; ++r)
             if ((RM >> r) & 1)
-                for (int j = 0; j < G; ++j) dot4(acc[r][j], wv[j], Xs[r * kPK4 + 16 * q[j] + kc]);
+                for (int j = 0; j < G; ++j) dot4(acc[r][j], wv[j], Xs[r * XSTR + 16 * q[j] + kc]);
     }
 }
 // rows r < NR of the W_hh2 window WIN (r % 3 == WIN) as a row mask
@@ -235,6 +241,11 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
     const float4* X0 = reinterpret_cast<const float4*>(lds + L_X0);
     const float4* X1 = reinterpret_cast<const float4*>(lds + L_X1);
     const float4* XH2 = reinterpret_cast<const float4*>(lds + L_XH2);
+    // x2 (fc1's input): its own rows below kPNR rows per group (L_X2); at kPNR rows formed in
+    // place over x1 in X0, after the hop-A arrival guard
+    constexpr bool X2B = NR < kPNR;
+    const float4* X2 = reinterpret_cast<const float4*>(lds + (X2B ? L_X2 : L_X0));
+    constexpr int X2S = X2B ? kPNR * kPK4 : kPK4;  // its row stride (float4)
     const int wave = tid >> 6;
     const bool wv_lo = wave < 4;  // waves 0-3: og < 16 (GRU2, hh2, fc2, fc3 <= 16 classes)
     // Per-step operands, issued right after the wave's last publish of the previous step
@@ -440,7 +451,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             }
             // this wave's reads of X0 (x1) are done (and its publishes issued): hop A may
             // overwrite X0 once all four GRU2 waves have arrived (x0_free below)
-            if (gate_a && (tid & 63) == 0)
+            if (!X2B && gate_a && (tid & 63) == 0)
                 __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(lds) + L_ARR, 1u, __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);  // (orders this wave's X0 reads before it)
         }
@@ -457,12 +468,14 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
         // X0 holds x1 until every GRU2 wave (0-3) has finished its stage-A products: a wave whose
         // hop-A poll completes early (its producer slots were ahead, e.g. at the launch's first
         // step) must not overwrite couples that a slower wave of this workgroup still reads
-        // (the sparse instances' per-lane work differs between waves). Waves 0-3 only; normally
+        // (the sparse instances' per-lane work differs between waves). Below kPNR rows per
+        // group x2 goes to its own rows (L_X2) and nothing is waited for; at kPNR rows (no spare
+        // row slots) it is formed in place after the arrival guard: waves 0-3 only, normally
         // satisfied on the first read.
         // (the counter is read once before the poll: when the four waves have arrived by then,
         // as they normally have, nothing is waited for after it)
         const unsigned arr_want = 4u * (unsigned)(t - a.t0 + 1);
-        const bool arr_early = wv_lo && __hip_atomic_load(reinterpret_cast<const unsigned*>(lds) + L_ARR,
+        const bool arr_early = X2B || !wv_lo || __hip_atomic_load(reinterpret_cast<const unsigned*>(lds) + L_ARR,
                                                           __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= arr_want;
         auto x0_free = [&]() {
             const unsigned want = arr_want;
@@ -490,29 +503,31 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
                 x0_free();
 #pragma unroll
                 for (int m = 0; m < NR; ++m) {  // x2 = x1 + h2 of the same couples (own writes)
-                    float2* x = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
+                    const float2* x = reinterpret_cast<const float2*>(lds + L_X0 + m * kPH) + tl;
+                    float2* y = reinterpret_cast<float2*>(lds + (X2B ? L_X2 + m * kPNR * kPH : L_X0 + m * kPH)) + tl;
                     const float2 h = *dst[m];
                     float2 v = *x;
                     v.x = p_add(v.x, h.x);
                     v.y = p_add(v.y, h.y);
-                    *x = v;
+                    *y = v;
                 }
             }
-        } else if (wv_lo) {  // x2 -> X0, polling the tagged pairs, one pass
+        } else if (wv_lo) {  // x2 -> X2 (X0 at kPNR rows), polling the tagged pairs, one pass
             unsigned off[NR];
             float2* dst[NR];
 #pragma unroll
             for (int m = 0; m < NR; ++m) {  // couple tl of row m
                 off[m] = (unsigned)(m * 5 * kPH + 2 * tl) * 8u;
-                dst[m] = reinterpret_cast<float2*>(lds + L_X0 + m * kPH) + tl;
+                dst[m] = reinterpret_cast<float2*>(lds + (X2B ? L_X2 + m * kPNR * kPH : L_X0 + m * kPH)) + tl;
             }
             x0_free();  // (the poll writes X0 itself)
             if (!poll_couples<NR>(xr, off, sA, seq, dst, a.ctl)) lds[L_FAIL] = 1.f;
         }
         __syncthreads();
         PSTAMP(2);
-        // fc1 / fc2: this thread's register rows wr[24..31] with the rows of X0, relu
-        auto mv1 = [&](float bias) {
+        // fc1 / fc2: this thread's register rows wr[24..31] with the rows of Xs (row stride XS), relu
+        auto mv1 = [&](float bias, const float4* Xs, auto xs_c) {
+            constexpr int XS = decltype(xs_c)::value;
             constexpr int QB = NR >= 4 ? 1 : kPQB1;
             float s0 = 0.f;
             v2f acc[NR];
@@ -521,7 +536,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
             if constexpr (SP) {
                 unsigned m[1] = {si.x >> 24}, p[1] = {si.z >> 16};
                 v2f (&a1)[NR][1] = *reinterpret_cast<v2f(*)[NR][1]>(&acc);
-                sp_products<NR, 1>(Wsp, X0, m, p, kc, a1);
+                sp_products<NR, 1, 0xF, XS>(Wsp, Xs, m, p, kc, a1);
             } else
 #pragma unroll
             for (int qb = 0; qb < 8; qb += QB) {
@@ -530,7 +545,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
 #pragma unroll
                 for (int r = 0; r < NR; ++r)
 #pragma unroll
-                    for (int q = 0; q < QB; ++q) xq[r][q] = X0[r * kPK4 + 16 * (qb + q) + kc];
+                    for (int q = 0; q < QB; ++q) xq[r][q] = Xs[r * XS + 16 * (qb + q) + kc];
 #pragma unroll
                 for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -546,7 +561,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
         };
         // ================= stage B: fc1 (waves 4-7, critical) ================================
         if (!gate_a) {
-            const float y = mv1(pc0);
+            const float y = mv1(pc0, X2, std::integral_constant<int, X2S>());
             // gh1 (hop A) must be in L2 before this wave's y1 can be seen
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_B * 4);
@@ -637,7 +652,7 @@ __device__ __forceinline__ void persist_body(const PersistArgs& a, float* lds, c
         PSTAMP(4);
         // ================= stage C: fc2 (waves 0-3, critical) ================================
         if (gate_a) {
-            const float y = mv1(pf2);
+            const float y = mv1(pf2, X0, std::integral_constant<int, kPK4>());
             if (kc < NR) bst_tag(y, seq, xr, o_y, XB_C * 4);
         } else {
             // P1 ring: operands of P1(t + 2), issued while no poll is in flight on this CU
