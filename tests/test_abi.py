@@ -108,3 +108,15 @@ def test_wide_exchange_layout_exhaustive():
     assert [lib.wrnn_debug_wide_layout(r) for r in range(1, 17)] == [0] * 16
     assert lib.wrnn_debug_wide_layout(0) == _abi.WRNN_ERR_INVALID
     assert lib.wrnn_debug_wide_layout(17) == _abi.WRNN_ERR_INVALID
+
+
+def test_fold_range_arguments_are_checked_on_the_host():
+    """wrnn_set_fold_ranges (the single-utterance fold split): a null handle is
+    refused with WRNN_ERR_INVALID without a device (ranges outside the folds, a count that does not
+    match the call and wrnn_generate's refusal: tests/test_gpu_fold_split.py)."""
+    from wavernn_amd import _abi
+    lib = _abi.load_library()
+    lo, hi = (ctypes.c_int * 1)(0), (ctypes.c_int * 1)(9)
+    assert lib.wrnn_set_fold_ranges(None, lo, hi, 1) == _abi.WRNN_ERR_INVALID
+    assert b'null handle' in lib.wrnn_last_error()
+    assert lib.wrnn_set_utt_streams(None, None, 0) == _abi.WRNN_ERR_INVALID
